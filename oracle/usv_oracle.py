@@ -1,0 +1,437 @@
+"""CPU restatement of romi2002/gym-usv's hot path — TEST INFRASTRUCTURE, NOT PRODUCT.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may
+import this module, and only as the checker (or the timed CPU baseline).  The product
+path (``gym-usv_amd``) never routes through it: it fails loudly without its HIP library.
+
+Parity pinning: this restatement is checked against golden vectors generated from the
+reference itself (``tests/golden/make_golden.py`` imports /root/reference read-only in the
+build container; fixtures ``tests/golden/*.npz``; checks in ``tests/test_oracle_golden.py``).
+
+Everything is float64 and batched over N envs (struct-of-arrays, one row per env), so the
+same code serves as the single-env oracle (N = 1) and as the 4096-env parity checker.
+Reference citations are ``path:line`` under the reference repo.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+# --------------------------------------------------------------------------- constants
+SENSOR_COUNT = 128                                   # simple_env.py:11
+SENSOR_SPAN = (2 / 3) * (2 * np.pi)                  # simple_env.py:12
+SENSOR_MAX_RANGE = 100.0                             # simple_env.py:13
+SENSOR_RES = SENSOR_SPAN / SENSOR_COUNT              # simple_env.py:14
+SENSOR_START = -np.pi * 2 / 3                        # usv_asmc_ca_env.py:420
+DT = 1 / 25                                          # simple_env.py:35
+BOUND_HI = 20.0                                      # simple_env.py:56 env_bounds = (0, 20)
+MAX_ACC = np.array([1.75, 0.0, 3.0])                 # simple_env.py:34 (+ [1] = 0 at :253)
+TARGET_NORM = np.array([np.pi, np.hypot(20.0, 20.0), 10.0, 10.0])   # simple_env.py:80
+LOOKAHEAD = (0.005 / 10) * 20                        # simple_env.py:146
+OBS_DIM = 15 + SENSOR_COUNT                          # simple_env.py:27
+TIME_LIMITS = {"usv-simple": 500, "usv-asmc-simple": 1000, "usv-asmc-v0": None}  # gym_usv/__init__.py
+
+# UsvAsmc coefficients (usv_asmc.py:7-41)
+X_U_DOT, Y_V_DOT, Y_R_DOT, N_V_DOT, N_R_DOT = -2.25, -23.13, -1.31, -16.41, -2.79
+YVV, YVR, YRV, YRR = -99.99, -5.49, -5.49, -8.8
+NVV, NVR, NRV, NRR = -5.49, -8.8, -8.8, -3.49
+MASS, IZ, B_TH, C_TH = 30.0, 4.1, 0.41, 0.78
+K_U, K_PSI, KMIN_U, KMIN_PSI = 0.1, 0.2, 0.05, 0.2
+K2_U, K2_PSI, MU_U, MU_PSI = 0.02, 0.1, 0.05, 0.1
+LAMBDA_U, LAMBDA_PSI = 0.001, 1.0
+F1, F2, F3 = 2.0, 2.0, 2.0
+H = 0.01                                             # usv_asmc.py:47 integral_step
+M_MAT = np.array([[MASS - X_U_DOT, 0, 0],
+                  [0, MASS - Y_V_DOT, 0 - Y_R_DOT],
+                  [0, 0 - N_V_DOT, IZ - N_R_DOT]])   # usv_asmc.py:172-174
+M_INV = np.linalg.inv(M_MAT)                         # constant; ref inverts per substep (:226)
+# Yv / Yr / Nv / Nr scale factors (usv_asmc.py:101-108)
+YV_K = 0.5 * (-40 * 1000) * (1.1 + 0.0045 * (1.01 / 0.09) - 0.1 * (0.27 / 0.09)
+                             + 0.016 * ((0.27 / 0.09) ** 2))
+YR_K = 6 * (-3.141592 * 1000) * 0.09 * 0.09 * 1.01
+NV_K = 0.06 * (-3.141592 * 1000) * 0.09 * 0.09 * 1.01
+NR_K = 0.02 * (-3.141592 * 1000) * 0.09 * 0.09 * 1.01 * 1.01
+
+# ASMC per-env persistent state layout (16 unique values; usv_asmc.py:43-49, :237-242)
+ASMC_FIELDS = ("psi_d_last", "o", "o_dot", "o_dot_dot",
+               "x_dot_last", "y_dot_last", "psi_dot_last",
+               "u_dot_last", "v_dot_last", "r_dot_last",
+               "e_u_last", "ka_dot_u_last", "ka_dot_psi_last",
+               "e_u_int", "ka_u", "ka_psi")
+ASMC_N = len(ASMC_FIELDS)
+
+
+def wrap_angle(a):
+    """simple_env.py:63-65 — atan2(sin, cos)."""
+    return np.arctan2(np.sin(a), np.cos(a))
+
+
+def wrap_once(e):
+    """Single wrap sign(e)(|e|-2pi) if |e|>pi (usv_asmc.py:120)."""
+    return np.where(np.abs(e) > np.pi, np.sign(e) * (np.abs(e) - 2 * np.pi), e)
+
+
+# --------------------------------------------------------------------------- lidar
+def lidar(px, py, psi, ox, oy, orad, n_obs):
+    """Batched 128-ray lidar.
+
+    Restates simple_env.py:203-226 -> usv_asmc_ca_env.py:411-437 (compute_sensor_measurments)
+    -> :500-519 (compute_obstacle_positions) -> :439-461 (_compute_sensor_distances).
+
+    The reference sorts obstacles by key d_j = |c_j - p| - r_j (argsort, :417) and, per ray,
+    takes the first obstacle in that order with proj >= 0, r^2 - perp^2 >= 0 and reading
+    proj - sqrt(r^2 - perp^2) < max range.  That is the hit obstacle with the smallest key
+    (the "min-key rule"), which is what this restatement and the HIP kernel compute.
+
+    Args: px, py, psi [N]; ox, oy, orad [N, cap] (entries j >= n_obs[i] ignored); n_obs [N].
+    Returns: keys [N, cap] (inf where padded), readings [N, 128].
+    """
+    px, py, psi = (np.asarray(a, dtype=np.float64) for a in (px, py, psi))
+    cap = ox.shape[1]
+    valid = np.arange(cap)[None, :] < np.asarray(n_obs)[:, None]
+    dx = ox - px[:, None]
+    dy = oy - py[:, None]
+    keys = np.where(valid, np.hypot(dx, dy) - orad, np.inf)             # simple_env.py:205-206
+    ang = (SENSOR_START + np.arange(SENSOR_COUNT) * SENSOR_RES)[None, :] + psi[:, None]  # :420-423
+    c, s = np.cos(ang)[:, :, None], np.sin(ang)[:, :, None]             # [N, 128, 1]
+    # inverse rotation of the obstacle offset, y mirrored (usv_asmc_ca_env.py:506-518)
+    proj = c * dx[:, None, :] + s * dy[:, None, :]
+    perp = s * dx[:, None, :] - c * dy[:, None, :]
+    delta = orad[:, None, :] ** 2 - perp * perp                         # :453
+    with np.errstate(invalid="ignore"):
+        reading = proj - np.sqrt(np.where(delta >= 0, delta, 0.0))      # :457
+    hit = valid[:, None, :] & (proj >= 0) & (delta >= 0) & (reading < SENSOR_MAX_RANGE)
+    kk = np.where(hit, keys[:, None, :], np.inf)
+    best = np.argmin(kk, axis=2)                                        # min-key == sorted first hit
+    any_hit = np.take_along_axis(hit, best[:, :, None], axis=2)[:, :, 0]
+    val = np.take_along_axis(reading, best[:, :, None], axis=2)[:, :, 0]
+    readings = np.where(any_hit, val, SENSOR_MAX_RANGE)
+    return keys, readings
+
+
+# --------------------------------------------------------------------------- ASMC
+class AsmcBatch:
+    """Batched restatement of ``UsvAsmc`` (usv_asmc.py:4-244), N independent controllers.
+
+    ``state`` is [N, 16] in ASMC_FIELDS order (psi_d_last, o, o', o'', eta_dot_last(3),
+    upsilon_dot_last(3), e_u_last, Ka_dot_u_last, Ka_dot_psi_last, e_u_int, Ka_u, Ka_psi).
+    The reference keeps o_last == o, o_dot_last == o_dot, o_dot_dot_last == o_dot_dot after
+    every substep (:89-92), so 16 values carry the full state.
+    """
+
+    def __init__(self, n):
+        self.state = np.zeros((n, ASMC_N))
+
+    def reset(self, idx=None):
+        if idx is None:
+            self.state[:] = 0.0
+        else:
+            self.state[idx] = 0.0
+
+    def compute(self, action, pos, vel, substeps=10):
+        """usv_asmc.py:53-244 with do_perturb=False. action [N,2] = (u_d, psi offset)."""
+        st = self.state
+        a0, a1 = action[:, 0].astype(np.float64), action[:, 1].astype(np.float64)
+        x, y, psi = pos[:, 0].copy(), pos[:, 1].copy(), pos[:, 2].copy()
+        u, v, r = vel[:, 0].copy(), vel[:, 1].copy(), vel[:, 2].copy()
+        (psi_d_last, o, o_d, o_dd, xd_l, yd_l, psid_l, ud_l, vd_l, rd_l,
+         e_u_last, kdu_l, kdp_l, e_u_int, ka_u, ka_psi) = (st[:, k].copy() for k in range(ASMC_N))
+        for _ in range(substeps):
+            speed = np.hypot(u, v)
+            beta = np.arcsin(v / (0.001 + speed))                         # :72
+            psi_d = psi + beta + a1                                       # :73-77
+            r_d = (psi_d - psi_d_last) / H                                # :84
+            psi_d_last = psi_d
+            o_dd_new = ((r_d - o) * F1 - F3 * o_d) * F2                   # :86
+            o_d_new = H * (o_dd_new + o_dd) / 2 + o_d                     # :87
+            o = H * (o_d_new + o_d) / 2 + o                               # :88 (uses old o_dot_last)
+            o_d, o_dd = o_d_new, o_dd_new
+            r_d = o                                                       # :89
+            fast = np.abs(u) > 1.2                                        # :95-99
+            xu = np.where(fast, 64.55, -25.0)
+            xuu = np.where(fast, -70.92, 0.0)
+            vmag = np.sqrt(u * u + v * v)
+            yv = YV_K * np.abs(v)                                         # :101-102
+            yr, nv, nr = YR_K * vmag, NV_K * vmag, NR_K * vmag            # :103-108
+            f_u = ((MASS - Y_V_DOT) * v * r + (xuu * np.abs(u) + xu * u)) / (MASS - X_U_DOT)  # :113
+            f_psi = ((-X_U_DOT + Y_V_DOT) * u * v + nr * r) / (IZ - N_R_DOT)                 # :115
+            e_psi = wrap_once(psi_d - psi)                                # :119-120
+            e_psi_dot = r_d - r                                           # :121
+            e_u = a0 - u                                                  # :128
+            e_u_int = H * (e_u + e_u_last) / 2 + e_u_int                  # :129
+            e_u_last = e_u
+            sig_u = e_u + LAMBDA_U * e_u_int                              # :133
+            sig_p = e_psi_dot + LAMBDA_PSI * e_psi                        # :134
+            kdu = np.where(ka_u > KMIN_U, K_U * np.sign(np.abs(sig_u) - MU_U), KMIN_U)       # :137
+            kdp = np.where(ka_psi > KMIN_PSI, K_PSI * np.sign(np.abs(sig_p) - MU_PSI), KMIN_PSI)
+            ka_u = H * (kdu + kdu_l) / 2 + ka_u                           # :143
+            ka_psi = H * (kdp + kdp_l) / 2 + ka_psi                       # :146
+            kdu_l, kdp_l = kdu, kdp
+            ua_u = -ka_u * np.sqrt(np.abs(sig_u)) * np.sign(sig_u) - K2_U * sig_u            # :150
+            ua_p = -ka_psi * np.sqrt(np.abs(sig_p)) * np.sign(sig_p) - K2_PSI * sig_p        # :151
+            tx = (LAMBDA_U * e_u - f_u - ua_u) * (MASS - X_U_DOT)         # :154 (/g_u)
+            tz = (LAMBDA_PSI * e_psi - f_psi - ua_p) * (IZ - N_R_DOT)     # :155
+            tport = tx / 2 + tz / B_TH                                    # :158
+            tstbd = tx / (2 * C_TH) - tz / (B_TH * C_TH)                  # :159
+            t0 = tport + C_TH * tstbd                                     # :176
+            t2 = 0.5 * B_TH * (tport - C_TH * tstbd)
+            # C(nu) = CRB + CA (:201-211), D = Dl - Dn (:213-223); rhs = T - C nu - D nu
+            c02 = -MASS * v + 2 * (Y_V_DOT * v + ((Y_R_DOT + N_V_DOT) / 2) * r)
+            c12 = MASS * u - X_U_DOT * MASS * u
+            c20 = MASS * v + 2 * ((-Y_V_DOT) * v - ((Y_R_DOT + N_V_DOT) / 2) * r)
+            c21 = -MASS * u + X_U_DOT * MASS * u
+            d00 = -xu - xuu * np.abs(u)
+            d11 = -yv - (YVV * np.abs(v) + YVR * np.abs(r))
+            d12 = -yr - (YRV * np.abs(v) + YRR * np.abs(r))
+            d21 = -nv - (NVV * np.abs(v) + NVR * np.abs(r))
+            d22 = -nr - (NRV * np.abs(v) + NRR * np.abs(r))
+            rhs0 = t0 - c02 * r - d00 * u
+            rhs1 = 0.0 - c12 * r - (d11 * v + d12 * r)
+            rhs2 = t2 - (c20 * u + c21 * v) - (d21 * v + d22 * r)
+            ud = M_INV[0, 0] * rhs0 + M_INV[0, 1] * rhs1 + M_INV[0, 2] * rhs2               # :226
+            vd = M_INV[1, 0] * rhs0 + M_INV[1, 1] * rhs1 + M_INV[1, 2] * rhs2
+            rd = M_INV[2, 0] * rhs0 + M_INV[2, 1] * rhs1 + M_INV[2, 2] * rhs2
+            u = H * (ud + ud_l) / 2 + u                                   # :228-229
+            v = H * (vd + vd_l) / 2 + v
+            r = H * (rd + rd_l) / 2 + r
+            ud_l, vd_l, rd_l = ud, vd, rd
+            cp, sp = np.cos(psi), np.sin(psi)                             # J(psi_old) :179-181
+            xd = cp * u - sp * v                                          # :233
+            yd = sp * u + cp * v
+            pd = r
+            x = H * (xd + xd_l) / 2 + x                                   # :234
+            y = H * (yd + yd_l) / 2 + y
+            psi = H * (pd + psid_l) / 2 + psi
+            xd_l, yd_l, psid_l = xd, yd, pd
+        self.state = np.stack([psi_d_last, o, o_d, o_dd, xd_l, yd_l, psid_l, ud_l, vd_l, rd_l,
+                               e_u_last, kdu_l, kdp_l, e_u_int, ka_u, ka_psi], axis=1)
+        return np.stack([x, y, psi], axis=1), np.stack([u, v, r], axis=1)
+
+
+# --------------------------------------------------------------------------- usv-simple
+class SimpleEnvBatch:
+    """Batched restatement of ``UsvSimpleEnv`` (simple_env.py:7-349), N envs.
+
+    Per-env state mirrors the reference attributes: position (x, y, psi), velocity (u, v, r),
+    last_action (3; [1] is always 0), progress, path_start / path_end, target_position,
+    max_action (3; [1] = 0 after reset), reference_velocity, obstacles (n, xy, radius) and
+    the stale ``sensor_data`` distances (:47, returned in the reset obs).
+    Each env owns a numpy Generator with gymnasium's seeding rule (PCG64(SeedSequence)).
+    """
+
+    obs_dim = OBS_DIM
+    act_dim = 2
+
+    def __init__(self, n, cap=32):
+        self.n, self.cap = n, cap
+        z = lambda *s: np.zeros((n,) + s)
+        self.position, self.velocity, self.last_action = z(3), z(3), z(3)
+        self.max_action = np.tile(np.array([3.0, 0.0, 3.0]), (n, 1))       # simple_env.py:32
+        self.ref_v = z()
+        self.progress = z()
+        self.path_start, self.path_end, self.target = z(2), z(2), z(2)
+        self.n_obs = np.zeros(n, dtype=np.int64)
+        self.ox, self.oy, self.orad = z(cap), z(cap), z(cap)
+        self.sensors = z(SENSOR_COUNT)                                    # stale scan (:47)
+        self.rngs = [None] * n
+
+    # ---- observation pieces (simple_env.py:67-96, 133-148) ----
+    def ye(self):
+        ak = np.arctan2(self.path_end[:, 1] - self.path_start[:, 1],
+                        self.path_end[:, 0] - self.path_start[:, 0])      # :134
+        return (-(self.position[:, 0] - self.path_start[:, 0]) * np.sin(ak)
+                + (self.position[:, 1] - self.path_start[:, 1]) * np.cos(ak))
+
+    def angle_to_target(self):
+        d = self.target - self.position[:, :2]                            # :68-69
+        return wrap_angle(np.arctan2(d[:, 1], d[:, 0]) - self.position[:, 2])
+
+    def target_state(self):
+        dist = np.hypot(self.position[:, 0] - self.target[:, 0],
+                        self.position[:, 1] - self.target[:, 1])          # :74
+        ts = np.stack([self.angle_to_target(), dist, self.ye(), self.ref_v], axis=1)
+        return ts / TARGET_NORM                                           # :79-80
+
+    def obs(self, action):
+        """_get_obs(action) (:91-96); ``action`` is [N,3]."""
+        act = action[:, [0, 2]] / self.max_action[:, [0, 2]]
+        kin = np.concatenate([self.max_action / 10, np.tile(MAX_ACC / 10, (self.n, 1))], axis=1)
+        return np.concatenate([self.velocity / 10, self.target_state(), act, kin,
+                               self.sensors / SENSOR_MAX_RANGE], axis=1).astype(np.float32)
+
+    def closest_point(self):
+        """_get_closest_point (:139-148)."""
+        x1, y1 = self.path_start[:, 0], self.path_start[:, 1]
+        dx = self.path_end[:, 0] - x1
+        dy = self.path_end[:, 1] - y1
+        a = (dy * (self.position[:, 1] - y1) + dx * (self.position[:, 0] - x1)) / (dx * dx + dy * dy)
+        a = a + LOOKAHEAD
+        a = np.clip(a, self.progress, 1)
+        return np.stack([x1 + a * dx, y1 + a * dy], axis=1), a
+
+    def reward(self, action):
+        """_get_reward (:150-201); action [N,3] is the new filtered action."""
+        min_sensor = self.sensors.min(axis=1)
+        collision = np.where(min_sensor < 0.2, -20.0, 0.0)                # :153-156
+        delta = np.abs(self.last_action - action).sum(axis=1)             # :160
+        angle = self.angle_to_target()
+        ye = self.ye()
+        k = 0.075
+        ye_r = np.maximum(np.exp(-np.abs(ye / k)), np.exp(-np.power(ye / k, 2)))   # :167-170
+        ang_r = np.exp(-np.abs(angle))                                    # :172
+        dact_r = -(delta / 2) * 0.15                                      # :176
+        vel_r = np.exp(-np.abs(np.hypot(self.velocity[:, 0], self.velocity[:, 1]) - self.ref_v)) * 0.05
+        return 0.0 + collision + ye_r + ang_r + vel_r + dact_r            # :181-186
+
+    # ---- reset (simple_env.py:228-308) ----
+    def reset_env(self, i, seed=None, options=None):
+        if seed is not None or self.rngs[i] is None:
+            self.rngs[i] = np.random.Generator(np.random.PCG64(np.random.SeedSequence(seed)))
+        g = self.rngs[i]
+        start = g.normal(scale=0.5, size=2) + np.array([BOUND_HI, BOUND_HI]) / 2      # :234
+        g.normal(start, scale=0.75); g.uniform(-np.pi, np.pi)                        # :236-237 discarded
+        psi = g.uniform(-np.pi, np.pi)                                               # :238
+        angle = g.uniform(-np.pi, np.pi)                                             # :241
+        dist = g.uniform(100, 110)                                                   # :242
+        self.path_start[i] = start
+        self.position[i] = [start[0], start[1], psi]
+        self.path_end[i] = start + np.array([np.cos(angle), np.sin(angle)]) * dist  # :243
+        self.target[i] = g.uniform(0, BOUND_HI, size=2)                              # :245
+        self.velocity[i] = g.uniform(0.0, 0.15, size=3)                              # :246
+        self.progress[i] = 0.0
+        ma = g.uniform(1.50, 3, size=3)                                              # :249
+        ma[2] = g.uniform(3, 6)                                                      # :250
+        self.ref_v[i] = g.uniform(0.75, ma[0])                                       # :251
+        ma[1] = 0.0                                                                  # :254
+        self.max_action[i] = ma
+        n = int(g.integers(15, 30))                                                  # :257
+        pos = g.uniform(0, BOUND_HI, size=(n, 2))                                    # :258
+        d_pos = np.hypot(start[0] - pos[:, 0], start[1] - pos[:, 1])
+        d_tgt = np.hypot(self.target[i, 0] - pos[:, 0], self.target[i, 1] - pos[:, 1])
+        keep = ~((d_pos < 0.5) | (d_tgt < 0.5))                                     # :261-268
+        pos = pos[keep]
+        if pos.shape[0] == 0:                                                        # :270-274
+            pos = g.uniform(0, BOUND_HI, size=(1, 2))
+        if options and options.get("place_obstacles_on_path"):                       # :276-288
+            k = options["place_obstacles_on_path"]
+            mag = g.uniform(0, np.hypot(BOUND_HI, BOUND_HI), k)
+            lx = g.normal(np.cos(angle) * mag + start[0], 1)
+            ly = g.normal(np.sin(angle) * mag + start[1], 1)
+            pos = np.concatenate([pos, np.stack([lx, ly], axis=1)])
+        n = pos.shape[0]
+        if n > self.cap:
+            raise ValueError(f"obstacle count {n} exceeds cap {self.cap}")
+        rad = g.uniform(0.15, 0.5, size=n)                                           # :290
+        self.n_obs[i] = n
+        self.ox[i], self.oy[i], self.orad[i] = 0.0, 0.0, 0.0
+        self.ox[i, :n], self.oy[i, :n], self.orad[i, :n] = pos[:, 0], pos[:, 1], rad
+
+    def reset(self, seeds=None, idx=None, options=None):
+        idx = range(self.n) if idx is None else idx
+        for k, i in enumerate(idx):
+            s = None if seeds is None else seeds[k]
+            self.reset_env(i, s, options)
+        return self.obs(np.zeros((self.n, 3)))                            # :302 (stale sensors)
+
+    # ---- step (simple_env.py:310-346) ----
+    def kinematics(self, action):
+        """Action scaling + filter + accel/speed clip + pose update (:311-324)."""
+        a3 = np.stack([action[:, 0], np.zeros(self.n), action[:, 1]], axis=1).astype(np.float64)
+        a3 = self.max_action * a3
+        a3 = 0.8 * self.last_action + 0.2 * a3
+        dv = np.clip(a3 - self.velocity, -MAX_ACC, MAX_ACC)
+        self.velocity = np.clip(self.velocity + dv, -self.max_action, self.max_action)
+        th = self.position[:, 2]
+        rot = np.stack([self.velocity[:, 0] * np.cos(th), self.velocity[:, 0] * np.sin(th),
+                        self.velocity[:, 2]], axis=1)
+        self.position = self.position + rot * DT
+        return a3
+
+    def step(self, action):
+        a3 = self.kinematics(np.asarray(action, dtype=np.float64))
+        return self._finish_step(a3)
+
+    def _finish_step(self, a3):
+        self.target, self.progress = self.closest_point()                 # :328
+        keys, self.sensors = lidar(self.position[:, 0], self.position[:, 1], self.position[:, 2],
+                                   self.ox, self.oy, self.orad, self.n_obs)   # :329
+        terminated = keys.min(axis=1) < 0.05                              # :334
+        pxy = self.position[:, :2]
+        truncated = np.any((pxy > BOUND_HI) | (pxy < 0), axis=1)          # :336
+        obs = self.obs(self.last_action)                                  # :338 (previous action)
+        rew = self.reward(a3)                                             # :339
+        self.last_action = a3                                             # :343
+        return obs, rew, terminated, truncated
+
+    # ---- state exchange with the HIP library (field names = include/usv_hip.h) ----
+    def get_state(self):
+        return {
+            "x": self.position[:, 0], "y": self.position[:, 1], "psi": self.position[:, 2],
+            "u": self.velocity[:, 0], "v": self.velocity[:, 1], "r": self.velocity[:, 2],
+            "last_u": self.last_action[:, 0], "last_r": self.last_action[:, 2],
+            "progress": self.progress,
+            "path_x0": self.path_start[:, 0], "path_y0": self.path_start[:, 1],
+            "path_x1": self.path_end[:, 0], "path_y1": self.path_end[:, 1],
+            "max_u": self.max_action[:, 0], "max_r": self.max_action[:, 2], "ref_v": self.ref_v,
+            "n_obs": self.n_obs, "obs_x": self.ox, "obs_y": self.oy, "obs_r": self.orad,
+            "sensor_last": self.sensors,
+        }
+
+
+class SimpleAsmcEnvBatch(SimpleEnvBatch):
+    """Batched ``UsvSimpleASMCEnv`` (simple_env_asmc.py:7-27): 2x UsvAsmc.compute (20 substeps
+    of 0.01 s) then ``UsvSimpleEnv.step(zeros(2))``.  Reset re-creates the controller
+    (zero state) and drops ``options`` (:14-16)."""
+
+    def __init__(self, n, cap=32):
+        super().__init__(n, cap)
+        self.asmc = AsmcBatch(n)
+
+    def reset_env(self, i, seed=None, options=None):
+        self.asmc.reset([i])
+        super().reset_env(i, seed, None)
+
+    def step(self, action):
+        action = np.asarray(action, dtype=np.float64)
+        for _ in range(2):                                                # simple_env_asmc.py:19-25
+            self.position, self.velocity = self.asmc.compute(action, self.position, self.velocity)
+        a3 = self.kinematics(np.zeros((self.n, 2)))                       # :27 super().step(zeros)
+        return self._finish_step(a3)
+
+    def get_state(self):
+        st = super().get_state()
+        st["asmc"] = self.asmc.state
+        return st
+
+
+# --------------------------------------------------------------------------- vector wrapper
+class OracleVectorEnv:
+    """N oracle envs behind the SB3/gymnasium vector semantics the HIP VectorEnv implements:
+    TimeLimit(max_episode_steps) (gym_usv/__init__.py:24-34) and same-step autoreset
+    (``final_obs`` = the terminal obs; the returned obs is the reset obs)."""
+
+    def __init__(self, env_id, num_envs, cap=32):
+        cls = {"usv-simple": SimpleEnvBatch, "usv-asmc-simple": SimpleAsmcEnvBatch}[env_id]
+        self.env = cls(num_envs, cap)
+        self.limit = TIME_LIMITS[env_id]
+        self.elapsed = np.zeros(num_envs, dtype=np.int64)
+
+    def reset(self, seeds):
+        self.elapsed[:] = 0
+        return self.env.reset(seeds)
+
+    def step(self, actions):
+        obs, rew, term, trunc = self.env.step(actions)
+        self.elapsed += 1
+        if self.limit:
+            trunc = trunc | (self.elapsed >= self.limit)
+        done = term | trunc
+        final_obs = obs.copy()
+        if done.any():
+            idx = np.flatnonzero(done)
+            self.env.reset(idx=idx)
+            self.elapsed[idx] = 0
+            obs = obs.copy()
+            obs[idx] = self.env.obs(np.zeros((self.env.n, 3)))[idx]
+        return obs, rew, term, trunc, final_obs, done

@@ -1,0 +1,165 @@
+"""Generate golden vectors from the reference (romi2002/gym-usv) — build container only.
+
+Run:  python tests/golden/make_golden.py      (needs /root/reference; writes tests/golden/*.npz)
+
+The reference is imported read-only through ``refharness`` (stand-ins for its uninstalled
+third-party imports).  Only inputs and outputs are stored; no
+reference source travels.  Fixtures:
+
+* ``asmc_compute.npz``   -- UsvAsmc.compute (usv_asmc.py:53-244) on injected random states,
+                            plus the three adapted reference KATs (tests/test_usv_asmc.py:8-37).
+* ``lidar.npz``          -- UsvAsmcCaEnv.compute_sensor_measurments (usv_asmc_ca_env.py:411-461)
+                            on random scenes as UsvSimpleEnv calls it (simple_env.py:203-226).
+* ``simple_traj.npz``    -- UsvSimpleEnv (usv-simple) seeded reset + random-action rollouts with
+                            TimeLimit + same-step autoreset (SB3 DummyVecEnv semantics).
+* ``asmc_simple_traj.npz`` -- the same for UsvSimpleASMCEnv (usv-asmc-simple).
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import refharness  # noqa: E402
+
+CAP = 32
+
+
+def gen_asmc(E):
+    from gym_usv.control.usv_asmc import UsvAsmc
+    rng = np.random.default_rng(1234)
+    n = 192
+    out = {k: [] for k in ("action", "pos_in", "vel_in", "last_in", "so_in", "aux_in",
+                           "pos_out", "vel_out", "last_out", "so_out", "aux_out")}
+    for i in range(n):
+        c = UsvAsmc()
+        # warm the controller from zero state with a random action so its internal state
+        # is realistic, then inject a perturbed state (covers both Xu regimes, Ka switches)
+        pos = np.array([rng.uniform(0, 20), rng.uniform(0, 20), rng.uniform(-4, 4)])
+        vel = np.array([rng.uniform(-0.5, 2.5), rng.uniform(-0.3, 0.3), rng.uniform(-1, 1)])
+        warm = np.array([rng.uniform(0.2, 1.0), rng.uniform(-1, 1)], dtype=np.float32)
+        for _ in range(int(rng.integers(0, 6))):
+            pos, vel, _ = c.compute(warm, pos, vel, False)
+        act = np.array([rng.uniform(0.2, 1.0), rng.uniform(-1, 1)], dtype=np.float32)
+        out["action"].append(act.astype(np.float64))
+        out["pos_in"].append(np.array(pos, dtype=np.float64))
+        out["vel_in"].append(np.array(vel, dtype=np.float64))
+        out["last_in"].append(np.array(c.last, dtype=np.float64))
+        out["so_in"].append(np.array(c.so_filter, dtype=np.float64))
+        out["aux_in"].append(np.array(c.aux_vars, dtype=np.float64))
+        p2, v2, _ = c.compute(act, pos, vel, False)
+        out["pos_out"].append(p2)
+        out["vel_out"].append(v2)
+        out["last_out"].append(np.array(c.last, dtype=np.float64))
+        out["so_out"].append(np.array(c.so_filter, dtype=np.float64))
+        out["aux_out"].append(np.array(c.aux_vars, dtype=np.float64))
+    res = {k: np.stack(v) for k, v in out.items()}
+    # adapted reference KATs: compute(a, p, v, False), 1000 calls from zero state
+    for name, a in (("kat_zero", [0, 0]), ("kat_fwd", [10, 0]), ("kat_rot", [0, 10])):
+        c = UsvAsmc()
+        pos, vel = np.zeros(3), np.zeros(3)
+        traj = []
+        for k in range(1000):
+            pos, vel, _ = c.compute(np.array(a, dtype=np.float64), pos, vel, False)
+            if k < 50 or k % 50 == 49:
+                traj.append(np.concatenate([pos, vel]))
+        res[name] = np.stack(traj)
+    np.savez_compressed(os.path.join(HERE, "asmc_compute.npz"), **res)
+    print("asmc_compute.npz", {k: v.shape for k, v in res.items()})
+
+
+def gen_lidar(E):
+    UsvAsmcCaEnv = E.UsvAsmcCaEnv
+    rng = np.random.default_rng(99)
+    n_scenes = 256
+    pos = np.zeros((n_scenes, 3))
+    ox, oy, orad = np.zeros((n_scenes, CAP)), np.zeros((n_scenes, CAP)), np.zeros((n_scenes, CAP))
+    nob = np.zeros(n_scenes, dtype=np.int64)
+    keys = np.full((n_scenes, CAP), np.inf)
+    sens = np.zeros((n_scenes, 128))
+    for i in range(n_scenes):
+        n = int(rng.integers(1, 30))
+        p = np.array([rng.uniform(-1, 21), rng.uniform(-1, 21), rng.uniform(-20, 20)])
+        xy = rng.uniform(0, 20, size=(n, 2))
+        r = rng.uniform(0.15, 0.5, size=n)
+        if i % 8 == 0:          # put the boat inside / touching an obstacle
+            xy[0] = p[:2] + rng.normal(scale=0.2, size=2)
+        sensor_count, span = 128, (2 / 3) * (2 * np.pi)
+        d = np.hypot(xy[:, 0] - p[0], xy[:, 1] - p[1]) - r      # simple_env.py:205-206
+        s = UsvAsmcCaEnv.compute_sensor_measurments(p, sensor_count, 100, r, span / sensor_count,
+                                                    xy[:, 0].reshape(-1, 1), xy[:, 1].reshape(-1, 1),
+                                                    n, d)
+        pos[i], nob[i] = p, n
+        ox[i, :n], oy[i, :n], orad[i, :n] = xy[:, 0], xy[:, 1], r
+        keys[i, :n] = d
+        sens[i] = s[:, 1]
+    np.savez_compressed(os.path.join(HERE, "lidar.npz"), pos=pos, ox=ox, oy=oy, orad=orad,
+                        n_obs=nob, keys=keys, sensors=sens)
+    print("lidar.npz", n_scenes)
+
+
+def snapshot(env):
+    n = env.obstacle_n
+    ox, oy, r = np.zeros(CAP), np.zeros(CAP), np.zeros(CAP)
+    ox[:n], oy[:n], r[:n] = env.obstacle_positions[:, 0], env.obstacle_positions[:, 1], env.obstacle_radius
+    return dict(position=np.array(env.position, dtype=np.float64),
+                velocity=np.array(env.velocity, dtype=np.float64),
+                last_action=np.array(env.last_action, dtype=np.float64),
+                progress=float(env.progress), path_start=np.array(env.path_start),
+                path_end=np.array(env.path_end), target=np.array(env.target_position),
+                max_action=np.array(env.max_action, dtype=np.float64),
+                ref_v=float(env.reference_velocity), n_obs=int(n), ox=ox, oy=oy, orad=r,
+                sensors=np.array(env.sensor_data[:, 1], dtype=np.float64))
+
+
+def gen_traj(E, cls, fname, limit, n_env=8, T=96):
+    """Per env: seeded reset, then T random-action steps under TimeLimit(limit) with
+    same-step autoreset (SB3 DummyVecEnv: reset() with no seed continues the stream)."""
+    rng = np.random.default_rng(7)
+    acts = np.stack([rng.uniform([0.2, -1], [1, 1], size=(T, 2)) for _ in range(n_env)]).astype(np.float32)
+    seeds = np.arange(n_env) + 1000
+    obs0 = np.zeros((n_env, 143), np.float32)
+    obs = np.zeros((n_env, T, 143), np.float32)
+    fobs = np.zeros((n_env, T, 143), np.float32)
+    rew = np.zeros((n_env, T))
+    term = np.zeros((n_env, T), bool)
+    trunc = np.zeros((n_env, T), bool)
+    st0 = []
+    for e in range(n_env):
+        env = cls(render_mode=None)
+        o, _ = env.reset(seed=int(seeds[e]))
+        obs0[e] = o
+        st0.append(snapshot(env))
+        elapsed = 0
+        for t in range(T):
+            o, r, te, tr, _ = env.step(acts[e, t])
+            elapsed += 1
+            tr = bool(tr) or (limit is not None and elapsed >= limit)
+            fobs[e, t], rew[e, t], term[e, t], trunc[e, t] = o, r, bool(te), tr
+            if te or tr:
+                o, _ = env.reset()
+                elapsed = 0
+            obs[e, t] = o
+    st = {f"init_{k}": np.stack([np.asarray(s[k]) for s in st0]) for k in st0[0]}
+    np.savez_compressed(os.path.join(HERE, fname), seeds=seeds, actions=acts, obs0=obs0, obs=obs,
+                        final_obs=fobs, reward=rew, terminated=term, truncated=trunc,
+                        limit=-1 if limit is None else limit, **st)
+    print(fname, "episodes ended:", int((term | trunc).sum()), "terminated:", int(term.sum()))
+
+
+def main():
+    refharness.load_reference()
+    import gym_usv.envs as E
+    gen_asmc(E)
+    gen_lidar(E)
+    gen_traj(E, E.UsvSimpleEnv, "simple_traj.npz", 500, n_env=8, T=256)
+    gen_traj(E, E.UsvSimpleASMCEnv, "asmc_simple_traj.npz", 1000, n_env=6, T=160)
+    # short time limit variant exercises TimeLimit truncation + autoreset path
+    gen_traj(E, E.UsvSimpleEnv, "simple_traj_tl.npz", 20, n_env=4, T=64)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,80 @@
+"""Pin the CPU oracle (oracle/usv_oracle.py) against golden vectors generated from the
+reference itself (tests/golden/make_golden.py).  CPU only."""
+import numpy as np
+import pytest
+
+from oracle import usv_oracle as O
+
+
+def test_lidar_matches_reference(golden):
+    g = golden("lidar.npz")
+    p = g["pos"]
+    keys, sens = O.lidar(p[:, 0], p[:, 1], p[:, 2], g["ox"], g["oy"], g["orad"], g["n_obs"])
+    np.testing.assert_allclose(keys, g["keys"], rtol=0, atol=1e-12)
+    np.testing.assert_allclose(sens, g["sensors"], rtol=0, atol=1e-10)
+    # coverage: hits, misses and negative readings (boat inside an obstacle) all present
+    assert (g["sensors"] == 100).any() and (g["sensors"] < 100).any() and (g["sensors"] < 0).any()
+
+
+def test_asmc_single_compute_matches_reference(golden):
+    g = golden("asmc_compute.npz")
+    n = g["action"].shape[0]
+    a = O.AsmcBatch(n)
+    so, last, aux = g["so_in"], g["last_in"], g["aux_in"]
+    # so_filter = [psi_d_last, o_dd_last, o_d_last, o_last, o, o_d, o_dd] (usv_asmc.py:58)
+    np.testing.assert_array_equal(so[:, 3], so[:, 4])
+    a.state = np.concatenate([so[:, [0, 4, 5, 6]], last, aux], axis=1)
+    pos, vel = a.compute(g["action"], g["pos_in"], g["vel_in"])
+    np.testing.assert_allclose(pos, g["pos_out"], rtol=1e-11, atol=1e-11)
+    np.testing.assert_allclose(vel, g["vel_out"], rtol=1e-11, atol=1e-11)
+    ref_state = np.concatenate([g["so_out"][:, [0, 4, 5, 6]], g["last_out"], g["aux_out"]], axis=1)
+    np.testing.assert_allclose(a.state, ref_state, rtol=1e-10, atol=1e-10)
+
+
+@pytest.mark.parametrize("name", ["kat_zero", "kat_fwd", "kat_rot"])
+def test_asmc_reference_kats(golden, name):
+    """Adapted reference tests (tests/test_usv_asmc.py:8-37): 1000 compute() calls."""
+    g = golden("asmc_compute.npz")
+    act = {"kat_zero": [0, 0], "kat_fwd": [10, 0], "kat_rot": [0, 10]}[name]
+    a = O.AsmcBatch(1)
+    pos, vel = np.zeros((1, 3)), np.zeros((1, 3))
+    traj = []
+    for k in range(1000):
+        pos, vel = a.compute(np.array([act], dtype=np.float64), pos, vel)
+        if k < 50 or k % 50 == 49:
+            traj.append(np.concatenate([pos[0], vel[0]]))
+    traj = np.stack(traj)
+    # first 300 calls pinned tightly; after that ulp differences (constant M^-1 instead of a
+    # per-substep inv, fused C/D products) get amplified through sign() switches (chaotic)
+    np.testing.assert_allclose(traj[:55], g[name][:55], rtol=1e-9, atol=1e-9)
+    if name == "kat_zero":
+        assert np.allclose(traj[-1], 0)
+    elif name == "kat_fwd":
+        assert traj[-1, 0] > 10 and np.all(np.abs(traj[-1, 1:3]) < 1) and traj[-1, 3] > 1
+    else:
+        assert traj[-1, 2] > 5
+
+
+@pytest.mark.parametrize("fname,env_id", [("simple_traj.npz", "usv-simple"),
+                                          ("simple_traj_tl.npz", "usv-simple"),
+                                          ("asmc_simple_traj.npz", "usv-asmc-simple")])
+def test_trajectories_match_reference(golden, fname, env_id):
+    g = golden(fname)
+    n, T = g["actions"].shape[:2]
+    venv = O.OracleVectorEnv(env_id, n)
+    if int(g["limit"]) > 0:
+        venv.limit = int(g["limit"])
+    obs = venv.reset([int(s) for s in g["seeds"]])
+    np.testing.assert_allclose(obs, g["obs0"], rtol=1e-6, atol=1e-6)
+    e = venv.env
+    np.testing.assert_allclose(e.position, g["init_position"], atol=1e-13)
+    np.testing.assert_array_equal(e.n_obs, g["init_n_obs"])
+    np.testing.assert_allclose(e.ox, g["init_ox"], atol=1e-13)
+    np.testing.assert_allclose(e.orad, g["init_orad"], atol=1e-13)
+    for t in range(T):
+        obs, rew, term, trunc, fobs, done = venv.step(g["actions"][:, t])
+        np.testing.assert_array_equal(term, g["terminated"][:, t], err_msg=f"t={t}")
+        np.testing.assert_array_equal(trunc, g["truncated"][:, t], err_msg=f"t={t}")
+        np.testing.assert_allclose(rew, g["reward"][:, t], rtol=1e-9, atol=1e-9, err_msg=f"t={t}")
+        np.testing.assert_allclose(fobs, g["final_obs"][:, t], rtol=1e-6, atol=1e-6, err_msg=f"t={t}")
+        np.testing.assert_allclose(obs, g["obs"][:, t], rtol=1e-6, atol=1e-6, err_msg=f"t={t}")
