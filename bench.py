@@ -1,0 +1,207 @@
+"""Benchmark: env-steps/s of the batched HIP USV step at 65 536 envs per GPU (BASELINE.json).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--envs 65536] [--env-id usv-simple]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+A "step" is one launch of the fused step kernel over every env of the rank (config C3:
+usv-simple, 65 536 envs, random actions in [0.2,1]x[-1,1], in-kernel TimeLimit + same-step
+autoreset).  Actions for all K timed steps are generated on the device before the timed
+region (inputs resident in HBM).  Multi-GPU: one process per GPU, envs sharded by global id
+(env_id_offset = rank * N), no collective on the step path (weak scaling); the only
+collectives are the barrier and the max-over-ranks of the elapsed time.
+
+Rank 0 prints one JSON line: value = all ranks' env-steps / max-rank time, plus
+  roofline:     algorithmic bytes per launch / mean kernel duration (HIP events around sampled
+                launches on the env's stream) vs 8 TB/s; traffic from the committed rocprofv3
+                PMC summary (profiles/pmc_summary.json) when it matches the workload.
+  cpu_baseline: the CPU oracle (per-env NumPy restatement of the reference step, oracle/) timed
+                on this host's cores for a bounded sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import multiprocessing as mp
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "gym-usv_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level table)
+METRIC = "env-steps/sec at 65 536 parallel envs; 1/2/4/8 MI355X scaling"
+
+
+# --------------------------------------------------------------------------- byte model
+def algorithmic_bytes_per_env_step(env_id, mean_obs, precision="f32"):
+    """Bytes one env-step must move (DESIGN.md 'Algorithmic bytes'): action in, obs/reward/flags
+    out, dynamic state read+write, obstacle read (x, y, r per obstacle).  Reset traffic excluded."""
+    w = 4 if precision == "f32" else 8
+    act, obs, rew, flags = 8, 143 * 4, w, 2
+    state_rd = 16 * w + 2 * 4          # 16 real fields + n_obs + elapsed
+    state_wr = 9 * w + 2 * 4           # pose, velocity, last action, progress + elapsed, scan flag
+    obst = 3 * w * mean_obs
+    asmc = 2 * 16 * w if env_id == "usv-asmc-simple" else 0
+    return act + obs + rew + flags + state_rd + state_wr + obst + asmc
+
+
+# --------------------------------------------------------------------------- CPU baseline
+def _cpu_worker(args):
+    env_id, seconds, seed = args
+    os.environ.setdefault("OMP_NUM_THREADS", "1")
+    import numpy as np
+    from oracle import usv_oracle as O
+    venv = O.OracleVectorEnv(env_id, 1)
+    venv.reset([seed])
+    rng = np.random.default_rng(seed)
+    n, t0 = 0, time.perf_counter()
+    while True:
+        venv.step(rng.uniform([0.2, -1], [1, 1], size=(1, 2)).astype(np.float32))
+        n += 1
+        if n % 32 == 0 and time.perf_counter() - t0 >= seconds:
+            break
+    return n, time.perf_counter() - t0
+
+
+def cpu_baseline(env_id, seconds, procs):
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(procs) as pool:
+        res = pool.map(_cpu_worker, [(env_id, seconds, 1000 + i) for i in range(procs)])
+    steps = sum(r[0] for r in res)
+    rate = sum(r[0] / r[1] for r in res)
+    return {"value": round(rate, 1), "unit": "env-steps/s", "cores": procs, "kind": "port",
+            "sample": f"{procs} single-threaded processes x 1 env x ~{seconds:.0f}s of random-action "
+                      f"{env_id} steps with TimeLimit+autoreset ({steps} env-steps total); "
+                      "oracle/usv_oracle.py per-env float64 NumPy restatement of the reference step"}
+
+
+# --------------------------------------------------------------------------- main
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10000)
+    ap.add_argument("--warmup", type=int, default=200)
+    ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
+    ap.add_argument("--env-id", default="usv-simple", choices=["usv-simple", "usv-asmc-simple"])
+    ap.add_argument("--precision", default="f32", choices=["f32", "f64"])
+    ap.add_argument("--lidar", default="brute", choices=["brute", "window"])
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-procs", type=int, default=0, help="0 = min(16, available cores)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--event-every", type=int, default=8, help="time every k-th launch with HIP events")
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_summary.json"))
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    import gym_usv_amd
+    N, K, W = args.envs, args.steps, args.warmup
+    env = gym_usv_amd.make_vec(args.env_id, N, device=local, seed=args.seed, precision=args.precision,
+                               lidar=args.lidar, env_id_offset=rank * N)
+    env.reset(seed=args.seed)
+    mean_obs = float(env.get_field("n_obs").mean())
+
+    # actions for every timed step resident in HBM before timing (cycled pool if huge)
+    pool = max(1, min(K, (8 << 30) // (N * 8)))
+    gen = torch.Generator(device=dev).manual_seed(args.seed * 7919 + rank)
+    lo = torch.tensor([0.2, -1.0], device=dev)
+    span = torch.tensor([0.8, 2.0], device=dev)
+    acts = torch.rand((pool, N, 2), device=dev, generator=gen) * span + lo
+    obs = torch.empty((N, 143), device=dev)
+    fobs = torch.empty((N, 143), device=dev)
+    rew = torch.empty(N, device=dev, dtype=torch.float32 if args.precision == "f32" else torch.float64)
+    term = torch.empty(N, device=dev, dtype=torch.uint8)
+    trunc = torch.empty(N, device=dev, dtype=torch.uint8)
+    stream = torch.cuda.current_stream(dev)
+    sptr = stream.cuda_stream
+
+    def launch(k):
+        rc = env.step_raw(acts[k % pool], obs, rew, term, trunc, fobs, stream=sptr)
+        if rc != 0:
+            raise RuntimeError(gym_usv_amd.load_library().usv_last_error().decode())
+
+    for k in range(W):
+        launch(k)
+    n_ev = (K + args.event_every - 1) // args.event_every
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_ev)]
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(K):
+        if k % args.event_every == 0:
+            a, b = ev[k // args.event_every]
+            a.record(stream)
+            launch(W + k)
+            b.record(stream)
+        else:
+            launch(W + k)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+
+    if rank == 0:
+        total_env_steps = N * world * K
+        value = total_env_steps / elapsed
+        bpe = algorithmic_bytes_per_env_step(args.env_id, mean_obs, args.precision)
+        bytes_per_launch = bpe * N
+        achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
+        traffic = None
+        if os.path.exists(args.pmc):
+            try:
+                pmc = json.load(open(args.pmc))
+                key = f"{args.env_id}/{N}/{args.precision}/{args.lidar}"
+                if key in pmc:
+                    traffic = pmc[key]["hbm_bytes_per_launch"]
+            except Exception:
+                traffic = None
+        out = {
+            "metric": METRIC, "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world,
+            "steps": K, "warmup": W, "ms_per_step": round(elapsed / K * 1e3, 5),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": args.precision, "data": "synthetic (on-device uniform random actions, Philox env resets)",
+            "config": {"workload": f"C3: {args.env_id}, {N} envs per GPU, random-action rollout, "
+                                   f"in-kernel TimeLimit + same-step autoreset",
+                       "env_id": args.env_id, "envs_per_gpu": N, "global_envs": N * world,
+                       "parallelism": f"env-sharded x{world}, no step-path collective",
+                       "lidar": args.lidar, "mean_obstacles": round(mean_obs, 2)},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic, "kernel_ms": round(kern_ms, 5),
+                         "algorithmic_bytes_per_env_step": round(bpe, 1)},
+        }
+        if not args.no_cpu_baseline:
+            procs = args.cpu_procs or min(16, len(os.sched_getaffinity(0)))
+            out["cpu_baseline"] = cpu_baseline(args.env_id, args.cpu_seconds, procs)
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    env.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

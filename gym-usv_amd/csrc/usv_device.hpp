@@ -1,0 +1,238 @@
+// usv_device.hpp — device-side building blocks of the gfx950 USV step kernels.
+//
+// Everything here is per-env math written for one of two thread mappings:
+//   * lane-per-env  (dynamics, ASMC, reward, reset): struct-of-arrays state, one env per
+//                   wavefront lane, coalesced [field][N] loads/stores;
+//   * wave-per-env  (lidar + observation row): 64 lanes own 128 rays (2 per lane), the
+//                   env's obstacles are wave-uniform and broadcast with v_readlane.
+// Reference citations are path:line in romi2002/gym-usv.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace usv {
+
+// ----------------------------------------------------------------------------- constants
+constexpr int kSensors = 128;                      // simple_env.py:11
+constexpr int kObsDim = 143;                       // simple_env.py:27
+constexpr int kHdr = 15;                           // obs[0:15] (simple_env.py:96)
+constexpr int kAsmcN = 16;                         // unique UsvAsmc state values
+constexpr int kWave = 64;
+constexpr double kPi = 3.14159265358979323846;
+constexpr double kSensorMax = 100.0;               // simple_env.py:13
+constexpr double kDt = 1.0 / 25.0;                 // simple_env.py:35
+constexpr double kBound = 20.0;                    // simple_env.py:56
+constexpr double kMaxAccU = 1.75, kMaxAccR = 3.0;  // simple_env.py:34
+constexpr double kDiag = 28.284271247461902;       // hypot(20, 20), simple_env.py:80
+constexpr double kLookahead = (0.005 / 10) * 20;   // simple_env.py:146
+constexpr double kTermDist = 0.05;                 // simple_env.py:334
+constexpr double kCollDist = 0.2;                  // simple_env.py:155
+constexpr double kYeK = 0.075;                     // simple_env.py:166
+
+// UsvAsmc coefficients (usv_asmc.py:7-41)
+constexpr double X_U_DOT = -2.25, Y_V_DOT = -23.13, Y_R_DOT = -1.31, N_V_DOT = -16.41,
+                 N_R_DOT = -2.79;
+constexpr double YVV = -99.99, YVR = -5.49, YRV = -5.49, YRR = -8.8;
+constexpr double NVV = -5.49, NVR = -8.8, NRV = -8.8, NRR = -3.49;
+constexpr double MASS = 30.0, IZ = 4.1, B_TH = 0.41, C_TH = 0.78;
+constexpr double K_U = 0.1, K_PSI = 0.2, KMIN_U = 0.05, KMIN_PSI = 0.2;
+constexpr double K2_U = 0.02, K2_PSI = 0.1, MU_U = 0.05, MU_PSI = 0.1;
+constexpr double LAMBDA_U = 0.001, LAMBDA_PSI = 1.0;
+constexpr double F1 = 2.0, F2 = 2.0, F3 = 2.0;
+constexpr double H = 0.01;                         // usv_asmc.py:47
+// Yv / Yr / Nv / Nr scale factors (usv_asmc.py:101-108)
+constexpr double YV_K = 0.5 * (-40.0 * 1000.0) *
+    (1.1 + 0.0045 * (1.01 / 0.09) - 0.1 * (0.27 / 0.09) + 0.016 * ((0.27 / 0.09) * (0.27 / 0.09)));
+constexpr double YR_K = 6.0 * (-3.141592 * 1000.0) * 0.09 * 0.09 * 1.01;
+constexpr double NV_K = 0.06 * (-3.141592 * 1000.0) * 0.09 * 0.09 * 1.01;
+constexpr double NR_K = 0.02 * (-3.141592 * 1000.0) * 0.09 * 0.09 * 1.01 * 1.01;
+// M^-1 of M = [[m - Xu', 0, 0], [0, m - Yv', -Yr'], [0, -Nv', Iz - Nr']] (usv_asmc.py:172-174);
+// constant, so inverted in closed form here instead of per substep (:226).
+constexpr double M00 = MASS - X_U_DOT, M11 = MASS - Y_V_DOT, M12 = -Y_R_DOT, M21 = -N_V_DOT,
+                 M22 = IZ - N_R_DOT;
+constexpr double MDET = M11 * M22 - M12 * M21;
+constexpr double MI00 = 1.0 / M00, MI11 = M22 / MDET, MI12 = -M12 / MDET, MI21 = -M21 / MDET,
+                 MI22 = M11 / MDET;
+
+// ----------------------------------------------------------------------------- math shims
+__device__ __forceinline__ float  m_sin(float x)  { return sinf(x); }
+__device__ __forceinline__ double m_sin(double x) { return sin(x); }
+__device__ __forceinline__ float  m_cos(float x)  { return cosf(x); }
+__device__ __forceinline__ double m_cos(double x) { return cos(x); }
+__device__ __forceinline__ void m_sincos(float x, float* s, float* c) { sincosf(x, s, c); }
+__device__ __forceinline__ void m_sincos(double x, double* s, double* c) { sincos(x, s, c); }
+__device__ __forceinline__ float  m_atan2(float y, float x)  { return atan2f(y, x); }
+__device__ __forceinline__ double m_atan2(double y, double x) { return atan2(y, x); }
+__device__ __forceinline__ float  m_asin(float x)  { return asinf(x); }
+__device__ __forceinline__ double m_asin(double x) { return asin(x); }
+__device__ __forceinline__ float  m_sqrt(float x)  { return sqrtf(x); }
+__device__ __forceinline__ double m_sqrt(double x) { return sqrt(x); }
+__device__ __forceinline__ float  m_exp(float x)  { return expf(x); }
+__device__ __forceinline__ double m_exp(double x) { return exp(x); }
+__device__ __forceinline__ float  m_hypot(float x, float y)  { return hypotf(x, y); }
+__device__ __forceinline__ double m_hypot(double x, double y) { return hypot(x, y); }
+__device__ __forceinline__ float  m_abs(float x)  { return fabsf(x); }
+__device__ __forceinline__ double m_abs(double x) { return fabs(x); }
+
+template <typename T> __device__ __forceinline__ T m_clip(T x, T lo, T hi) {
+  // np.clip(x, lo, hi) == minimum(maximum(x, lo), hi)
+  x = x > lo ? x : lo;
+  return x < hi ? x : hi;
+}
+template <typename T> __device__ __forceinline__ T m_sign(T x) {   // np.sign: sign(0) = 0
+  return x > T(0) ? T(1) : (x < T(0) ? T(-1) : T(0));
+}
+template <typename T> __device__ __forceinline__ T wrap_once(T e) {  // usv_asmc.py:120
+  return m_abs(e) > T(kPi) ? m_sign(e) * (m_abs(e) - T(2 * kPi)) : e;
+}
+template <typename T> __device__ __forceinline__ T wrap_angle(T a) {  // simple_env.py:63-65
+  T s, c;
+  m_sincos(a, &s, &c);
+  return m_atan2(s, c);
+}
+
+// ----------------------------------------------------------------------------- wave helpers
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ float bcast(float v, int lane) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+__device__ __forceinline__ double bcast(double v, int lane) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), lane);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+template <typename T> __device__ __forceinline__ T wave_min(T v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const T o = __shfl_xor(v, off, kWave);
+    v = o < v ? o : v;
+  }
+  return v;
+}
+
+// ----------------------------------------------------------------------------- Philox RNG
+// Counter-based Philox4x32-10: key = run seed, counter = (global env id, episode, draw).
+// Resets are reproducible per (seed, global env id, episode) and independent of how the
+// envs are sharded over GPUs.  The reference draws from numpy PCG64 (simple_env.py:228-308);
+// parity of resets is distributional (tests/test_gpu_parity.py KS tests).
+struct Philox {
+  uint32_t c0, c1, c2, c3, k0, k1;
+  double spare;
+  bool has_spare;
+
+  __device__ Philox(uint64_t seed, uint64_t gid, uint32_t episode)
+      : c0((uint32_t)gid), c1((uint32_t)(gid >> 32)), c2(episode), c3(0),
+        k0((uint32_t)seed), k1((uint32_t)(seed >> 32)), spare(0.0), has_spare(false) {}
+
+  __device__ void block(uint32_t& o0, uint32_t& o1, uint32_t& o2, uint32_t& o3) {
+    uint32_t x0 = c0, x1 = c1, x2 = c2, x3 = c3, a = k0, b = k1;
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+      const uint32_t lo0 = 0xD2511F53u * x0, hi0 = __umulhi(0xD2511F53u, x0);
+      const uint32_t lo1 = 0xCD9E8D57u * x2, hi1 = __umulhi(0xCD9E8D57u, x2);
+      x0 = hi1 ^ x1 ^ a; x1 = lo1; x2 = hi0 ^ x3 ^ b; x3 = lo0;
+      a += 0x9E3779B9u; b += 0xBB67AE85u;
+    }
+    ++c3;
+    o0 = x0; o1 = x1; o2 = x2; o3 = x3;
+  }
+  // uniform double in [0, 1) with 53 random bits
+  __device__ double uniform() {
+    if (has_spare) { has_spare = false; return spare; }
+    uint32_t a, b, c, d;
+    block(a, b, c, d);
+    const double s = 1.0 / 9007199254740992.0;  // 2^-53
+    spare = (double)((((uint64_t)c << 32) | d) >> 11) * s;
+    has_spare = true;
+    return (double)((((uint64_t)a << 32) | b) >> 11) * s;
+  }
+  __device__ double uniform(double lo, double hi) { return lo + (hi - lo) * uniform(); }
+  __device__ double normal(double mean, double scale) {  // Box-Muller
+    const double u1 = 1.0 - uniform(), u2 = uniform();
+    return mean + scale * sqrt(-2.0 * log(u1)) * cos(2.0 * kPi * u2);
+  }
+  __device__ int integers(int lo, int hi) {  // [lo, hi)
+    int v = lo + (int)(uniform() * (double)(hi - lo));
+    return v < hi ? v : hi - 1;
+  }
+};
+
+// ----------------------------------------------------------------------------- ASMC
+// One UsvAsmc.compute substep (usv_asmc.py:56-242, do_perturb = False).  State `s` holds
+// the 16 unique values: psi_d_last, o, o', o'', eta_dot_last[3], upsilon_dot_last[3],
+// e_u_last, Ka_dot_u_last, Ka_dot_psi_last, e_u_int, Ka_u, Ka_psi.
+template <typename R>
+__device__ __forceinline__ void asmc_substep(R (&s)[kAsmcN], R a0, R a1, R& x, R& y, R& psi,
+                                             R& u, R& v, R& r) {
+  const R speed = m_hypot(u, v);
+  const R beta = m_asin(v / (R(0.001) + speed));                          // :72
+  const R psi_d = psi + beta + a1;                                         // :73-77
+  R r_d = (psi_d - s[0]) / R(H);                                           // :84
+  s[0] = psi_d;
+  const R o_dd = ((r_d - s[1]) * R(F1) - R(F3) * s[2]) * R(F2);            // :86
+  const R o_d = R(H) * (o_dd + s[3]) / R(2) + s[2];                        // :87
+  const R o = R(H) * (o_d + s[2]) / R(2) + s[1];                           // :88
+  s[1] = o; s[2] = o_d; s[3] = o_dd;
+  r_d = o;                                                                 // :89
+  const bool fast = m_abs(u) > R(1.2);                                     // :95-99
+  const R xu = fast ? R(64.55) : R(-25.0);
+  const R xuu = fast ? R(-70.92) : R(0.0);
+  const R vmag = m_sqrt(u * u + v * v);
+  const R yv = R(YV_K) * m_abs(v);                                         // :101-102
+  const R yr = R(YR_K) * vmag, nv = R(NV_K) * vmag, nr = R(NR_K) * vmag;  // :103-108
+  const R f_u = (R(MASS - Y_V_DOT) * v * r + (xuu * m_abs(u) + xu * u)) / R(MASS - X_U_DOT);  // :113
+  const R f_psi = (R(-X_U_DOT + Y_V_DOT) * u * v + nr * r) / R(IZ - N_R_DOT);                 // :115
+  const R e_psi = wrap_once(psi_d - psi);                                  // :119-120
+  const R e_psi_dot = r_d - r;                                             // :121
+  const R e_u = a0 - u;                                                    // :128
+  s[13] = R(H) * (e_u + s[10]) / R(2) + s[13];                             // :129 e_u_int
+  s[10] = e_u;
+  const R sig_u = e_u + R(LAMBDA_U) * s[13];                               // :133
+  const R sig_p = e_psi_dot + R(LAMBDA_PSI) * e_psi;                       // :134
+  const R kdu = s[14] > R(KMIN_U) ? R(K_U) * m_sign(m_abs(sig_u) - R(MU_U)) : R(KMIN_U);       // :137
+  const R kdp = s[15] > R(KMIN_PSI) ? R(K_PSI) * m_sign(m_abs(sig_p) - R(MU_PSI)) : R(KMIN_PSI);
+  s[14] = R(H) * (kdu + s[11]) / R(2) + s[14];                             // :143
+  s[15] = R(H) * (kdp + s[12]) / R(2) + s[15];                             // :146
+  s[11] = kdu; s[12] = kdp;
+  const R ua_u = -s[14] * m_sqrt(m_abs(sig_u)) * m_sign(sig_u) - R(K2_U) * sig_u;    // :150
+  const R ua_p = -s[15] * m_sqrt(m_abs(sig_p)) * m_sign(sig_p) - R(K2_PSI) * sig_p;  // :151
+  const R tx = (R(LAMBDA_U) * e_u - f_u - ua_u) * R(MASS - X_U_DOT);      // :154
+  const R tz = (R(LAMBDA_PSI) * e_psi - f_psi - ua_p) * R(IZ - N_R_DOT);  // :155
+  const R tport = tx / R(2) + tz / R(B_TH);                                // :158
+  const R tstbd = tx / R(2 * C_TH) - tz / R(B_TH * C_TH);                  // :159
+  const R t0 = tport + R(C_TH) * tstbd;                                    // :176
+  const R t2 = R(0.5 * B_TH) * (tport - R(C_TH) * tstbd);
+  // rhs = T - C(nu) nu - D(nu) nu with C = CRB + CA (:201-211), D = Dl - Dn (:213-223)
+  const R c02 = R(-MASS) * v + R(2) * (R(Y_V_DOT) * v + R((Y_R_DOT + N_V_DOT) / 2) * r);
+  const R c12 = R(MASS) * u - R(X_U_DOT * MASS) * u;
+  const R c20 = R(MASS) * v + R(2) * (R(-Y_V_DOT) * v - R((Y_R_DOT + N_V_DOT) / 2) * r);
+  const R c21 = R(-MASS) * u + R(X_U_DOT * MASS) * u;
+  const R av = m_abs(v), ar = m_abs(r);
+  const R d00 = -xu - xuu * m_abs(u);
+  const R d11 = -yv - (R(YVV) * av + R(YVR) * ar);
+  const R d12 = -yr - (R(YRV) * av + R(YRR) * ar);
+  const R d21 = -nv - (R(NVV) * av + R(NVR) * ar);
+  const R d22 = -nr - (R(NRV) * av + R(NRR) * ar);
+  const R rhs0 = t0 - c02 * r - d00 * u;
+  const R rhs1 = R(0) - c12 * r - (d11 * v + d12 * r);
+  const R rhs2 = t2 - (c20 * u + c21 * v) - (d21 * v + d22 * r);
+  const R ud = R(MI00) * rhs0;                                             // :226
+  const R vd = R(MI11) * rhs1 + R(MI12) * rhs2;
+  const R rd = R(MI21) * rhs1 + R(MI22) * rhs2;
+  u = R(H) * (ud + s[7]) / R(2) + u;                                       // :228-229
+  v = R(H) * (vd + s[8]) / R(2) + v;
+  r = R(H) * (rd + s[9]) / R(2) + r;
+  s[7] = ud; s[8] = vd; s[9] = rd;
+  R sp, cp;
+  m_sincos(psi, &sp, &cp);                                                 // J(psi_old) :179
+  const R xd = cp * u - sp * v, yd = sp * u + cp * v, pd = r;              // :233
+  x = R(H) * (xd + s[4]) / R(2) + x;                                       // :234
+  y = R(H) * (yd + s[5]) / R(2) + y;
+  psi = R(H) * (pd + s[6]) / R(2) + psi;
+  s[4] = xd; s[5] = yd; s[6] = pd;
+}
+
+}  // namespace usv

@@ -1,0 +1,754 @@
+// usv_kernels.hip — gfx950 kernels + C-ABI (include/usv_hip.h) for the batched USV
+// path-following environment (usv-simple / usv-asmc-simple).
+//
+// One step = ONE launch over all envs.  A 256-thread block owns EPB consecutive envs:
+//   phase 1  lane-per-env  (wave 0): [ASMC 2x10 substeps] + kinematics + closest point +
+//            cross-track error + target features + reward terms + truncation; SoA state
+//            loads/stores are coalesced [field][N]; results for phase 2 go to LDS.
+//   phase 2  wave-per-env  (all 4 waves): obstacle keys (lane j = obstacle j), termination,
+//            128-ray lidar (lane l = rays l, l+64; obstacle data broadcast by v_readlane so
+//            the ray loop is wave-uniform), min sensor, and the whole 572-B observation row
+//            written by contiguous lanes (coalesced).
+//   phase 3  lane-per-env  (wave 0): reward, flags, and in-kernel masked autoreset
+//            (Philox, no host round trip) for done envs.
+// Reference: see include/usv_hip.h for the file:line each entry point replaces.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "usv_device.hpp"
+#include "usv_hip.h"
+
+namespace usv {
+
+template <typename R> struct alignas(4 * sizeof(R)) R4 { R x, y, z, w; };
+
+enum RealField {
+  F_X, F_Y, F_PSI, F_U, F_V, F_R, F_LAST_U, F_LAST_R, F_PROGRESS,
+  F_PX0, F_PY0, F_PX1, F_PY1, F_MAX_U, F_MAX_R, F_REF_V, F_NREAL
+};
+
+template <typename R> struct State {
+  R* f[F_NREAL];           // [field][N]
+  int32_t* n_obs;          // [N]
+  int32_t* elapsed;        // [N]
+  int32_t* episode;        // [N]
+  int32_t* scan_valid;     // [N]
+  R4<R>* obst;             // [N][cap] (x, y, r, r*r)
+  R* sensor_last;          // [N][128]
+  R* asmc;                 // [16][N]
+  const R* ray_co;         // [128] cos(start + i*res)
+  const R* ray_so;         // [128] sin(start + i*res)
+  int N, cap, limit, autoreset;
+  uint64_t seed, gid0;
+};
+
+template <typename R> struct IO {
+  const float* act;        // [N][2]
+  float* obs;              // [N][143]
+  R* rew;                  // [N]
+  uint8_t* term;           // [N]
+  uint8_t* trunc;          // [N]
+  float* fobs;             // [N][143] or null
+  const uint8_t* mask;     // [N] or null (reset kernel)
+};
+
+constexpr int kBlock = 256;
+constexpr int kWaves = kBlock / kWave;
+constexpr int kEPB = 64;   // envs per block
+
+template <typename R> __device__ __forceinline__ R big() { return R(1e30); }
+
+// obs[0:15] = [velocity/10, target_state(4), last_action[[0,2]]/max_action[[0,2]],
+//              max_action/10, max_acceleration/10]   (simple_env.py:72-96)
+template <typename R>
+__device__ __forceinline__ void make_header(float (&h)[kHdr], R u, R v, R r, R angle, R dist,
+                                            R ye, R refv, R act_u, R act_r, R mu, R mr) {
+  h[0] = (float)(u / R(10)); h[1] = (float)(v / R(10)); h[2] = (float)(r / R(10));
+  h[3] = (float)(angle / R(kPi)); h[4] = (float)(dist / R(kDiag));
+  h[5] = (float)(ye / R(10)); h[6] = (float)(refv / R(10));
+  h[7] = (float)(act_u / mu); h[8] = (float)(act_r / mr);
+  h[9] = (float)(mu / R(10)); h[10] = 0.0f; h[11] = (float)(mr / R(10));
+  h[12] = (float)(kMaxAccU / 10.0); h[13] = 0.0f; h[14] = (float)(kMaxAccR / 10.0);
+}
+
+// --------------------------------------------------------------------------- reset
+// In-kernel episode reset of env e (lane-per-env), distributionally identical to
+// UsvSimpleEnv.reset (simple_env.py:228-308); writes the reset-obs header.
+// last_action is NOT reset (reference quirk), sensor_data stays stale.
+template <typename R, int MODE>
+__device__ void reset_env(const State<R>& S, int e, float (&hdr)[kHdr]) {
+  const int ep = S.episode[e];
+  Philox g(S.seed, S.gid0 + (uint64_t)e, (uint32_t)ep);
+  const double sx = g.normal(kBound / 2, 0.5), sy = g.normal(kBound / 2, 0.5);   // :234-235
+  const double psi = g.uniform(-kPi, kPi);                                        // :238
+  const double ang = g.uniform(-kPi, kPi), dist = g.uniform(100.0, 110.0);        // :241-242
+  const double ex = sx + cos(ang) * dist, ey = sy + sin(ang) * dist;              // :243
+  const double tx = g.uniform(0.0, kBound), ty = g.uniform(0.0, kBound);          // :245
+  const double u = g.uniform(0.0, 0.15), v = g.uniform(0.0, 0.15), r = g.uniform(0.0, 0.15);  // :246
+  const double mu = g.uniform(1.5, 3.0);                                          // :249
+  const double mr = g.uniform(3.0, 6.0);                                          // :250
+  const double refv = g.uniform(0.75, mu);                                        // :251
+  const int n = g.integers(15, 30);                                               // :257
+  R4<R>* ob = S.obst + (size_t)e * S.cap;
+  int k = 0;
+  for (int j = 0; j < n; ++j) {                                                   // :258-268
+    const double ox = g.uniform(0.0, kBound), oy = g.uniform(0.0, kBound);
+    if (hypot(sx - ox, sy - oy) < 0.5 || hypot(tx - ox, ty - oy) < 0.5) continue;
+    const double rad = g.uniform(0.15, 0.5);                                      // :290
+    ob[k++] = R4<R>{R(ox), R(oy), R(rad), R(rad) * R(rad)};
+  }
+  if (k == 0) {                                                                   // :270-274
+    const double ox = g.uniform(0.0, kBound), oy = g.uniform(0.0, kBound);
+    const double rad = g.uniform(0.15, 0.5);
+    ob[k++] = R4<R>{R(ox), R(oy), R(rad), R(rad) * R(rad)};
+  }
+  for (int j = k; j < S.cap; ++j) ob[j] = R4<R>{R(0), R(0), R(0), R(0)};
+  const R x = R(sx), y = R(sy), p = R(psi);
+  S.f[F_X][e] = x; S.f[F_Y][e] = y; S.f[F_PSI][e] = p;
+  S.f[F_U][e] = R(u); S.f[F_V][e] = R(v); S.f[F_R][e] = R(r);
+  S.f[F_PROGRESS][e] = R(0);
+  S.f[F_PX0][e] = x; S.f[F_PY0][e] = y; S.f[F_PX1][e] = R(ex); S.f[F_PY1][e] = R(ey);
+  S.f[F_MAX_U][e] = R(mu); S.f[F_MAX_R][e] = R(mr); S.f[F_REF_V][e] = R(refv);
+  S.n_obs[e] = k;
+  S.elapsed[e] = 0;
+  S.episode[e] = ep + 1;
+  S.scan_valid[e] = 0;
+  if (MODE == USV_MODE_ASMC_SIMPLE) {                                             // simple_env_asmc.py:15
+#pragma unroll
+    for (int i = 0; i < kAsmcN; ++i) S.asmc[(size_t)i * S.N + e] = R(0);
+  }
+  // reset obs: _get_obs(zeros(3)) with the random target_position (:302, :72-80)
+  const R rtx = R(tx), rty = R(ty);
+  const R angle = wrap_angle(m_atan2(rty - y, rtx - x) - p);
+  const R dst = m_hypot(x - rtx, y - rty);
+  const R dx = R(ex) - x, dy = R(ey) - y;
+  const R ak = m_atan2(dy, dx);
+  R sak, cak;
+  m_sincos(ak, &sak, &cak);
+  const R ye = -(x - x) * sak + (y - y) * cak;                                    // :133-137
+  make_header<R>(hdr, R(u), R(v), R(r), angle, dst, ye, R(refv), R(0), R(0), R(mu), R(mr));
+}
+
+// --------------------------------------------------------------------------- phase 1
+// UsvSimpleEnv.step kinematics..reward terms (simple_env.py:310-346); for usv-asmc-simple
+// first 2x UsvAsmc.compute (simple_env_asmc.py:18-27) and then step(zeros(2)).
+template <typename R, int MODE>
+__device__ void env_dynamics(const State<R>& S, int e, float a_u, float a_r, float (&hdr)[kHdr],
+                             R& px, R& py, R& ppsi, R& partial, bool& trunc) {
+  R x = S.f[F_X][e], y = S.f[F_Y][e], psi = S.f[F_PSI][e];
+  R u = S.f[F_U][e], v = S.f[F_V][e], r = S.f[F_R][e];
+  if (MODE == USV_MODE_ASMC_SIMPLE) {
+    R s[kAsmcN];
+#pragma unroll
+    for (int i = 0; i < kAsmcN; ++i) s[i] = S.asmc[(size_t)i * S.N + e];
+    const R c0 = R(a_u), c1 = R(a_r);
+    for (int k = 0; k < 20; ++k) asmc_substep<R>(s, c0, c1, x, y, psi, u, v, r);
+#pragma unroll
+    for (int i = 0; i < kAsmcN; ++i) S.asmc[(size_t)i * S.N + e] = s[i];
+    a_u = 0.0f;                                                                   // step(zeros(2))
+    a_r = 0.0f;
+  }
+  const R lu = S.f[F_LAST_U][e], lr = S.f[F_LAST_R][e];
+  const R mu = S.f[F_MAX_U][e], mr = S.f[F_MAX_R][e], refv = S.f[F_REF_V][e];
+  // action = max_action * insert(action, 1, 0); filtered 0.8/0.2 (:311-317)
+  const R a3u = R(0.8) * lu + R(0.2) * (mu * R(a_u));
+  const R a3r = R(0.8) * lr + R(0.2) * (mr * R(a_r));
+  // per-step acceleration clip, then speed clip; max_action[1] = 0 pins v to 0 (:320-321)
+  const R dvu = m_clip(a3u - u, R(-kMaxAccU), R(kMaxAccU));
+  const R dvr = m_clip(a3r - r, R(-kMaxAccR), R(kMaxAccR));
+  u = m_clip(u + dvu, -mu, mu);
+  v = R(0);
+  r = m_clip(r + dvr, -mr, mr);
+  R sp, cp;
+  m_sincos(psi, &sp, &cp);
+  x = x + (u * cp) * R(kDt);                                                      // :322-324
+  y = y + (u * sp) * R(kDt);
+  psi = psi + r * R(kDt);
+  // _get_closest_point (:139-148)
+  const R x0 = S.f[F_PX0][e], y0 = S.f[F_PY0][e];
+  const R dx = S.f[F_PX1][e] - x0, dy = S.f[F_PY1][e] - y0;
+  R a = (dy * (y - y0) + dx * (x - x0)) / (dx * dx + dy * dy);
+  a = a + R(kLookahead);
+  a = m_clip(a, S.f[F_PROGRESS][e], R(1));
+  const R tx = x0 + a * dx, ty = y0 + a * dy;
+  // _get_ye (:133-137), _get_angle_to_target (:67-69), distance (:74)
+  const R ak = m_atan2(dy, dx);
+  R sak, cak;
+  m_sincos(ak, &sak, &cak);
+  const R ye = -(x - x0) * sak + (y - y0) * cak;
+  const R angle = wrap_angle(m_atan2(ty - y, tx - x) - psi);
+  const R dist = m_hypot(x - tx, y - ty);
+  const int el = S.elapsed[e] + 1;
+  trunc = (x > R(kBound)) | (x < R(0)) | (y > R(kBound)) | (y < R(0)) |   // :336
+          (S.limit > 0 && el >= S.limit);                                 // TimeLimit
+  make_header<R>(hdr, u, v, r, angle, dist, ye, refv, lu, lr, mu, mr);   // obs uses PREVIOUS action
+  // _get_reward without the collision term (:150-186)
+  const R dact = m_abs(lu - a3u) + m_abs(lr - a3r);
+  const R yk = ye / R(kYeK);
+  const R e1 = m_exp(-m_abs(yk)), e2 = m_exp(-(yk * yk));
+  const R ye_r = e1 > e2 ? e1 : e2;
+  const R ang_r = m_exp(-m_abs(angle));
+  const R vel_r = m_exp(-m_abs(m_hypot(u, v) - refv)) * R(0.05);
+  const R dact_r = -(dact / R(2)) * R(0.15);
+  partial = ye_r + ang_r + vel_r + dact_r;
+  S.f[F_X][e] = x; S.f[F_Y][e] = y; S.f[F_PSI][e] = psi;
+  S.f[F_U][e] = u; S.f[F_V][e] = v; S.f[F_R][e] = r;
+  S.f[F_LAST_U][e] = a3u; S.f[F_LAST_R][e] = a3r;
+  S.f[F_PROGRESS][e] = a;
+  S.elapsed[e] = el;
+  S.scan_valid[e] = 1;
+  px = x; py = y; ppsi = psi;
+}
+
+// --------------------------------------------------------------------------- lidar
+// 128-ray lidar of env e at pose (px, py, psi), wave-per-env.  Lane l owns rays l, l+64.
+// Restates compute_sensor_measurments / compute_obstacle_positions /
+// _compute_sensor_distances (usv_asmc_ca_env.py:411-461, 500-519): per ray, the hit
+// obstacle with the smallest key d_j = |c_j - p| - r_j (== first hit in argsort order).
+template <typename R>
+__device__ __forceinline__ void ray_test(R c, R s, R jdx, R jdy, R jr2, R jk, R& bk, R& bp, R& bd) {
+  const R proj = jdx * c + jdy * s;        // obstacle x in the ray frame (:506-517)
+  const R perp = jdx * s - jdy * c;        // obstacle y, mirrored (:518)
+  const R delta = jr2 - perp * perp;       // :453
+  bool hit = (proj >= R(0)) & (delta >= R(0));
+  if (hit && !(proj < R(kSensorMax))) hit = (proj - m_sqrt(delta)) < R(kSensorMax);  // :458
+  if (hit & (jk < bk)) { bk = jk; bp = proj; bd = delta; }
+}
+
+template <typename R>
+__device__ void lidar_wave(const State<R>& S, int e, int n, R px, R py, R psi, R co0, R so0,
+                           R co1, R so1, R& rd0, R& rd1, R& min_key) {
+  const int l = lane_id();
+  R dx = R(0), dy = R(0), r2 = R(0), key = big<R>();
+  if (l < n) {                                                // lane j = obstacle j
+    const R4<R> o = S.obst[(size_t)e * S.cap + l];
+    dx = o.x - px;
+    dy = o.y - py;
+    r2 = o.w;
+    key = m_sqrt(dx * dx + dy * dy) - o.z;                    // simple_env.py:205-206
+  }
+  min_key = wave_min(key);
+  R sp, cp;
+  m_sincos(psi, &sp, &cp);
+  // ray angle = psi + (start + i*res) (usv_asmc_ca_env.py:420-423), by rotation
+  const R c0 = cp * co0 - sp * so0, s0 = sp * co0 + cp * so0;
+  const R c1 = cp * co1 - sp * so1, s1 = sp * co1 + cp * so1;
+  R bk0 = big<R>(), bp0 = R(0), bd0 = R(0);
+  R bk1 = big<R>(), bp1 = R(0), bd1 = R(0);
+  for (int j = 0; j < n; ++j) {                               // wave-uniform obstacle loop
+    const R jdx = bcast(dx, j), jdy = bcast(dy, j), jr2 = bcast(r2, j), jk = bcast(key, j);
+    ray_test(c0, s0, jdx, jdy, jr2, jk, bk0, bp0, bd0);
+    ray_test(c1, s1, jdx, jdy, jr2, jk, bk1, bp1, bd1);
+  }
+  rd0 = bk0 < big<R>() ? bp0 - m_sqrt(bd0) : R(kSensorMax);   // :457-459, else max range
+  rd1 = bk1 < big<R>() ? bp1 - m_sqrt(bd1) : R(kSensorMax);
+}
+
+template <typename R> struct Scratch {
+  float hdr[kHdr][kEPB + 1];
+  R px[kEPB], py[kEPB], psi[kEPB], partial[kEPB], msens[kEPB];
+  uint8_t trunc[kEPB], term[kEPB];
+};
+
+// --------------------------------------------------------------------------- step kernel
+template <typename R, int MODE>
+__global__ __launch_bounds__(kBlock) void step_kernel(State<R> S, IO<R> io) {
+  __shared__ Scratch<R> sh;
+  const int tid = threadIdx.x;
+  const int wave = tid / kWave;
+  const int l = lane_id();
+  const int e0 = blockIdx.x * kEPB;
+
+  // ---- phase 1: lane-per-env dynamics
+  if (tid < kEPB) {
+    const int e = e0 + tid;
+    if (e < S.N) {
+      const float2 a = reinterpret_cast<const float2*>(io.act)[e];
+      float hdr[kHdr];
+      R px, py, psi, partial;
+      bool trunc;
+      env_dynamics<R, MODE>(S, e, a.x, a.y, hdr, px, py, psi, partial, trunc);
+#pragma unroll
+      for (int i = 0; i < kHdr; ++i) sh.hdr[i][tid] = hdr[i];
+      sh.px[tid] = px; sh.py[tid] = py; sh.psi[tid] = psi;
+      sh.partial[tid] = partial;
+      sh.trunc[tid] = trunc;
+    }
+  }
+  __syncthreads();
+
+  // ---- phase 2: wave-per-env lidar + observation rows
+  const R co0 = S.ray_co[l], so0 = S.ray_so[l], co1 = S.ray_co[l + 64], so1 = S.ray_so[l + 64];
+  for (int k = wave; k < kEPB; k += kWaves) {
+    const int e = e0 + k;
+    if (e >= S.N) break;
+    const int n = S.n_obs[e];
+    R rd0, rd1, min_key;
+    lidar_wave<R>(S, e, n, sh.px[k], sh.py[k], sh.psi[k], co0, so0, co1, so1, rd0, rd1, min_key);
+    const bool term = min_key < R(kTermDist);                  // simple_env.py:334
+    const bool done = term || sh.trunc[k];
+    const R ms = wave_min(rd0 < rd1 ? rd0 : rd1);              // simple_env.py:153
+    if (l == 0) { sh.term[k] = term; sh.msens[k] = ms; }
+    const float s0 = (float)(rd0 / R(kSensorMax)), s1 = (float)(rd1 / R(kSensorMax));  // :82-83
+    const bool reset_now = done && S.autoreset == USV_AUTORESET_SAME_STEP;
+    float* row = io.obs + (size_t)e * kObsDim;
+    row[kHdr + l] = s0;                                        // stale scan is kept by reset
+    row[kHdr + 64 + l] = s1;
+    if (!reset_now && l < kHdr) row[l] = sh.hdr[l][k];
+    if (done && io.fobs) {
+      float* f = io.fobs + (size_t)e * kObsDim;
+      f[kHdr + l] = s0;
+      f[kHdr + 64 + l] = s1;
+      if (l < kHdr) f[l] = sh.hdr[l][k];
+    }
+    if (reset_now) {
+      S.sensor_last[(size_t)e * kSensors + l] = rd0;
+      S.sensor_last[(size_t)e * kSensors + 64 + l] = rd1;
+    }
+  }
+  __syncthreads();
+
+  // ---- phase 3: lane-per-env reward, flags, autoreset
+  if (tid < kEPB) {
+    const int e = e0 + tid;
+    if (e < S.N) {
+      const R coll = sh.msens[tid] < R(kCollDist) ? R(-20) : R(0);   // simple_env.py:153-156
+      io.rew[e] = coll + sh.partial[tid];
+      const bool term = sh.term[tid], trunc = sh.trunc[tid];
+      io.term[e] = term;
+      io.trunc[e] = trunc;
+      if ((term || trunc) && S.autoreset == USV_AUTORESET_SAME_STEP) {
+        float hdr[kHdr];
+        reset_env<R, MODE>(S, e, hdr);
+        float* row = io.obs + (size_t)e * kObsDim;
+#pragma unroll
+        for (int i = 0; i < kHdr; ++i) row[i] = hdr[i];
+      }
+    }
+  }
+  (void)l;
+}
+
+// --------------------------------------------------------------------------- reset kernel
+// Explicit (host-requested) reset of masked envs.  Reset obs = new header + the stale
+// sensor_data: the scan at the last stepped pose (recomputed when that pose is still the
+// current one, else the stored one; zeros for a never-stepped env), simple_env.py:302.
+template <typename R, int MODE>
+__global__ __launch_bounds__(kBlock) void reset_kernel(State<R> S, IO<R> io) {
+  const int tid = threadIdx.x;
+  const int wave = tid / kWave;
+  const int l = lane_id();
+  const int e0 = blockIdx.x * kEPB;
+  const R co0 = S.ray_co[l], so0 = S.ray_so[l], co1 = S.ray_co[l + 64], so1 = S.ray_so[l + 64];
+  for (int k = wave; k < kEPB; k += kWaves) {
+    const int e = e0 + k;
+    if (e >= S.N) break;
+    if (io.mask && !io.mask[e]) continue;
+    R rd0, rd1;
+    R* last = S.sensor_last + (size_t)e * kSensors;
+    if (S.scan_valid[e]) {
+      R mk;
+      lidar_wave<R>(S, e, S.n_obs[e], S.f[F_X][e], S.f[F_Y][e], S.f[F_PSI][e], co0, so0, co1,
+                    so1, rd0, rd1, mk);
+      last[l] = rd0;
+      last[64 + l] = rd1;
+    } else {
+      rd0 = last[l];
+      rd1 = last[64 + l];
+    }
+    float* row = io.obs + (size_t)e * kObsDim;
+    row[kHdr + l] = (float)(rd0 / R(kSensorMax));
+    row[kHdr + 64 + l] = (float)(rd1 / R(kSensorMax));
+  }
+  __syncthreads();
+  if (tid < kEPB) {
+    const int e = e0 + tid;
+    if (e < S.N && (!io.mask || io.mask[e])) {
+      float hdr[kHdr];
+      reset_env<R, MODE>(S, e, hdr);
+      float* row = io.obs + (size_t)e * kObsDim;
+#pragma unroll
+      for (int i = 0; i < kHdr; ++i) row[i] = hdr[i];
+    }
+  }
+}
+
+}  // namespace usv
+
+// ============================================================================= host side
+using namespace usv;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                 \
+  do {                                                                                \
+    hipError_t _e = (expr);                                                           \
+    if (_e != hipSuccess)                                                             \
+      return fail(USV_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(_e));      \
+  } while (0)
+
+struct FieldDesc { const char* name; int is_int; };
+const FieldDesc kFields[USV_FIELD_COUNT] = {
+    {"x", 0}, {"y", 0}, {"psi", 0}, {"u", 0}, {"v", 0}, {"r", 0}, {"last_u", 0}, {"last_r", 0},
+    {"progress", 0}, {"path_x0", 0}, {"path_y0", 0}, {"path_x1", 0}, {"path_y1", 0},
+    {"max_u", 0}, {"max_r", 0}, {"ref_v", 0}, {"n_obs", 1}, {"elapsed", 1}, {"episode", 1},
+    {"scan_valid", 1}, {"obs_x", 0}, {"obs_y", 0}, {"obs_r", 0}, {"sensor_last", 0}, {"asmc", 0}};
+
+struct Handle {
+  usv_config cfg;
+  int device;
+  void* slab = nullptr;
+  State<float> sf{};
+  State<double> sd{};
+};
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (prev != dev) (void)hipSetDevice(dev);
+  }
+  ~DeviceGuard() {
+    int cur;
+    if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+  }
+};
+
+template <typename R>
+int carve(Handle* h, State<R>& S) {
+  const size_t N = (size_t)h->cfg.num_envs, cap = (size_t)h->cfg.obstacle_cap;
+  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  const size_t bytes = F_NREAL * al(N * sizeof(R)) + 4 * al(N * 4) + al(N * cap * sizeof(R4<R>)) +
+                       al(N * kSensors * sizeof(R)) + al((size_t)kAsmcN * N * sizeof(R)) +
+                       2 * al(kSensors * sizeof(R));
+  HIP_TRY(hipMalloc(&h->slab, bytes));
+  HIP_TRY(hipMemset(h->slab, 0, bytes));
+  char* p = (char*)h->slab;
+  auto take = [&](size_t b) { char* q = p; p += al(b); return (void*)q; };
+  for (int i = 0; i < F_NREAL; ++i) S.f[i] = (R*)take(N * sizeof(R));
+  S.n_obs = (int32_t*)take(N * 4);
+  S.elapsed = (int32_t*)take(N * 4);
+  S.episode = (int32_t*)take(N * 4);
+  S.scan_valid = (int32_t*)take(N * 4);
+  S.obst = (R4<R>*)take(N * cap * sizeof(R4<R>));
+  S.sensor_last = (R*)take(N * kSensors * sizeof(R));
+  S.asmc = (R*)take((size_t)kAsmcN * N * sizeof(R));
+  R* co = (R*)take(kSensors * sizeof(R));
+  R* so = (R*)take(kSensors * sizeof(R));
+  S.ray_co = co;
+  S.ray_so = so;
+  S.N = h->cfg.num_envs;
+  S.cap = h->cfg.obstacle_cap;
+  S.limit = h->cfg.max_episode_steps;
+  S.autoreset = h->cfg.autoreset;
+  S.seed = h->cfg.seed;
+  S.gid0 = h->cfg.env_id_offset;
+  // ray offsets start + i*res (usv_asmc_ca_env.py:420), cos/sin in float64 on the host
+  std::vector<R> hc(kSensors), hs(kSensors);
+  const double span = (2.0 / 3.0) * (2.0 * kPi), res = span / kSensors;
+  for (int i = 0; i < kSensors; ++i) {
+    const double a = -kPi * 2.0 / 3.0 + i * res;
+    hc[i] = (R)std::cos(a);
+    hs[i] = (R)std::sin(a);
+  }
+  HIP_TRY(hipMemcpy(co, hc.data(), kSensors * sizeof(R), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(so, hs.data(), kSensors * sizeof(R), hipMemcpyHostToDevice));
+  // reference __init__ defaults: max_action = [3, 0, 3] (simple_env.py:32)
+  std::vector<R> three(N, (R)3);
+  HIP_TRY(hipMemcpy(S.f[F_MAX_U], three.data(), N * sizeof(R), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(S.f[F_MAX_R], three.data(), N * sizeof(R), hipMemcpyHostToDevice));
+  return USV_OK;
+}
+
+template <typename R>
+int launch_step(Handle* h, State<R>& S, const float* act, float* obs, void* rew, uint8_t* term,
+                uint8_t* trunc, float* fobs, hipStream_t st) {
+  IO<R> io{act, obs, (R*)rew, term, trunc, fobs, nullptr};
+  const dim3 grid((S.N + kEPB - 1) / kEPB), block(kBlock);
+  if (h->cfg.mode == USV_MODE_SIMPLE)
+    hipLaunchKernelGGL((step_kernel<R, USV_MODE_SIMPLE>), grid, block, 0, st, S, io);
+  else
+    hipLaunchKernelGGL((step_kernel<R, USV_MODE_ASMC_SIMPLE>), grid, block, 0, st, S, io);
+  HIP_TRY(hipGetLastError());
+  return USV_OK;
+}
+
+template <typename R>
+int launch_reset(Handle* h, State<R>& S, const uint8_t* mask, float* obs, hipStream_t st) {
+  IO<R> io{nullptr, obs, nullptr, nullptr, nullptr, nullptr, mask};
+  const dim3 grid((S.N + kEPB - 1) / kEPB), block(kBlock);
+  if (h->cfg.mode == USV_MODE_SIMPLE)
+    hipLaunchKernelGGL((reset_kernel<R, USV_MODE_SIMPLE>), grid, block, 0, st, S, io);
+  else
+    hipLaunchKernelGGL((reset_kernel<R, USV_MODE_ASMC_SIMPLE>), grid, block, 0, st, S, io);
+  HIP_TRY(hipGetLastError());
+  return USV_OK;
+}
+
+int field_per_env(const Handle* h, int f) {
+  if (f >= USV_FIELD_OBS_X && f <= USV_FIELD_OBS_R) return h->cfg.obstacle_cap;
+  if (f == USV_FIELD_SENSOR_LAST) return kSensors;
+  if (f == USV_FIELD_ASMC) return kAsmcN;
+  return 1;
+}
+
+// host <-> device for one field; host side [N][per] float64 / int32
+template <typename R>
+int field_io(Handle* h, State<R>& S, int f, void* host, bool to_host) {
+  const size_t N = (size_t)S.N;
+  HIP_TRY(hipDeviceSynchronize());
+  if (f < F_NREAL) {
+    std::vector<R> tmp(N);
+    double* hd = (double*)host;
+    if (to_host) {
+      HIP_TRY(hipMemcpy(tmp.data(), S.f[f], N * sizeof(R), hipMemcpyDeviceToHost));
+      for (size_t i = 0; i < N; ++i) hd[i] = (double)tmp[i];
+    } else {
+      for (size_t i = 0; i < N; ++i) tmp[i] = (R)hd[i];
+      HIP_TRY(hipMemcpy(S.f[f], tmp.data(), N * sizeof(R), hipMemcpyHostToDevice));
+    }
+    return USV_OK;
+  }
+  if (f >= USV_FIELD_N_OBS && f <= USV_FIELD_SCAN_VALID) {
+    int32_t* d = f == USV_FIELD_N_OBS ? S.n_obs : f == USV_FIELD_ELAPSED ? S.elapsed
+               : f == USV_FIELD_EPISODE ? S.episode : S.scan_valid;
+    if (!to_host && f == USV_FIELD_N_OBS) {
+      const int32_t* hv = (const int32_t*)host;
+      for (size_t i = 0; i < N; ++i)
+        if (hv[i] < 0 || hv[i] > S.cap) return fail(USV_ERR_ARG, "n_obs out of [0, obstacle_cap]");
+    }
+    if (to_host) HIP_TRY(hipMemcpy(host, d, N * 4, hipMemcpyDeviceToHost));
+    else HIP_TRY(hipMemcpy(d, host, N * 4, hipMemcpyHostToDevice));
+    return USV_OK;
+  }
+  if (f >= USV_FIELD_OBS_X && f <= USV_FIELD_OBS_R) {
+    const size_t cnt = N * (size_t)S.cap;
+    std::vector<R4<R>> tmp(cnt);
+    HIP_TRY(hipMemcpy(tmp.data(), S.obst, cnt * sizeof(R4<R>), hipMemcpyDeviceToHost));
+    double* hd = (double*)host;
+    for (size_t i = 0; i < cnt; ++i) {
+      R4<R>& o = tmp[i];
+      R& c = f == USV_FIELD_OBS_X ? o.x : f == USV_FIELD_OBS_Y ? o.y : o.z;
+      if (to_host) hd[i] = (double)c;
+      else {
+        c = (R)hd[i];
+        if (f == USV_FIELD_OBS_R) o.w = o.z * o.z;
+      }
+    }
+    if (!to_host) HIP_TRY(hipMemcpy(S.obst, tmp.data(), cnt * sizeof(R4<R>), hipMemcpyHostToDevice));
+    return USV_OK;
+  }
+  if (f == USV_FIELD_SENSOR_LAST) {
+    const size_t cnt = N * kSensors;
+    std::vector<R> tmp(cnt);
+    double* hd = (double*)host;
+    if (to_host) {
+      HIP_TRY(hipMemcpy(tmp.data(), S.sensor_last, cnt * sizeof(R), hipMemcpyDeviceToHost));
+      for (size_t i = 0; i < cnt; ++i) hd[i] = (double)tmp[i];
+    } else {
+      for (size_t i = 0; i < cnt; ++i) tmp[i] = (R)hd[i];
+      HIP_TRY(hipMemcpy(S.sensor_last, tmp.data(), cnt * sizeof(R), hipMemcpyHostToDevice));
+    }
+    return USV_OK;
+  }
+  if (f == USV_FIELD_ASMC) {   // device [16][N], host [N][16]
+    const size_t cnt = N * kAsmcN;
+    std::vector<R> tmp(cnt);
+    double* hd = (double*)host;
+    if (to_host) {
+      HIP_TRY(hipMemcpy(tmp.data(), S.asmc, cnt * sizeof(R), hipMemcpyDeviceToHost));
+      for (size_t e = 0; e < N; ++e)
+        for (int i = 0; i < kAsmcN; ++i) hd[e * kAsmcN + i] = (double)tmp[(size_t)i * N + e];
+    } else {
+      for (size_t e = 0; e < N; ++e)
+        for (int i = 0; i < kAsmcN; ++i) tmp[(size_t)i * N + e] = (R)hd[e * kAsmcN + i];
+      HIP_TRY(hipMemcpy(S.asmc, tmp.data(), cnt * sizeof(R), hipMemcpyHostToDevice));
+    }
+    return USV_OK;
+  }
+  return fail(USV_ERR_ARG, "unknown field");
+}
+
+size_t field_bytes(const Handle* h, int f) {
+  return (size_t)h->cfg.num_envs * field_per_env(h, f) * (kFields[f].is_int ? 4 : 8);
+}
+
+Handle* as_handle(void* p) { return static_cast<Handle*>(p); }
+
+}  // namespace
+
+extern "C" {
+
+int usv_abi_version(void) { return USV_ABI_VERSION; }
+
+const char* usv_last_error(void) { return g_err.c_str(); }
+
+void usv_config_default(usv_config* cfg, int32_t mode, int32_t num_envs) {
+  if (!cfg) return;
+  std::memset(cfg, 0, sizeof(*cfg));
+  cfg->abi_version = USV_ABI_VERSION;
+  cfg->mode = mode;
+  cfg->precision = USV_F32;
+  cfg->num_envs = num_envs;
+  cfg->obstacle_cap = 32;
+  cfg->max_episode_steps = mode == USV_MODE_ASMC_SIMPLE ? 1000 : 500;   // gym_usv/__init__.py:27,33
+  cfg->autoreset = USV_AUTORESET_SAME_STEP;
+  cfg->lidar_algo = USV_LIDAR_BRUTE;
+  cfg->seed = 0;
+  cfg->env_id_offset = 0;
+}
+
+int usv_create(const usv_config* cfg, int32_t device, void** out) {
+  if (!cfg || !out) return fail(USV_ERR_ARG, "null argument");
+  *out = nullptr;
+  if (cfg->abi_version != USV_ABI_VERSION) return fail(USV_ERR_ABI, "abi_version mismatch");
+  if (cfg->mode != USV_MODE_SIMPLE && cfg->mode != USV_MODE_ASMC_SIMPLE)
+    return fail(USV_ERR_ARG, "unknown mode");
+  if (cfg->precision != USV_F32 && cfg->precision != USV_F64)
+    return fail(USV_ERR_ARG, "unknown precision");
+  if (cfg->num_envs <= 0) return fail(USV_ERR_ARG, "num_envs must be > 0");
+  if (cfg->obstacle_cap < 29 || cfg->obstacle_cap > 64)
+    return fail(USV_ERR_ARG, "obstacle_cap must be in [29, 64] (reference draws up to 29)");
+  if (cfg->autoreset != USV_AUTORESET_SAME_STEP && cfg->autoreset != USV_AUTORESET_DISABLED)
+    return fail(USV_ERR_ARG, "unknown autoreset mode");
+  if (cfg->lidar_algo != USV_LIDAR_BRUTE && cfg->lidar_algo != USV_LIDAR_WINDOW)
+    return fail(USV_ERR_ARG, "unknown lidar algorithm");
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  if (device < 0 || device >= ndev) return fail(USV_ERR_ARG, "bad device index");
+  DeviceGuard g(device);
+  Handle* h = new Handle();
+  h->cfg = *cfg;
+  h->device = device;
+  const int rc = cfg->precision == USV_F32 ? carve<float>(h, h->sf) : carve<double>(h, h->sd);
+  if (rc != USV_OK) {
+    if (h->slab) (void)hipFree(h->slab);
+    delete h;
+    return rc;
+  }
+  *out = h;
+  return USV_OK;
+}
+
+void usv_destroy(void* hp) {
+  Handle* h = as_handle(hp);
+  if (!h) return;
+  DeviceGuard g(h->device);
+  (void)hipDeviceSynchronize();
+  if (h->slab) (void)hipFree(h->slab);
+  delete h;
+}
+
+int usv_num_envs(void* hp) { return hp ? as_handle(hp)->cfg.num_envs : fail(USV_ERR_ARG, "null handle"); }
+int usv_obs_dim(void* hp) { return hp ? kObsDim : fail(USV_ERR_ARG, "null handle"); }
+int usv_reward_bytes(void* hp) {
+  return hp ? (as_handle(hp)->cfg.precision == USV_F64 ? 8 : 4) : fail(USV_ERR_ARG, "null handle");
+}
+
+int usv_seed(void* hp, uint64_t seed) {
+  Handle* h = as_handle(hp);
+  if (!h) return fail(USV_ERR_ARG, "null handle");
+  DeviceGuard g(h->device);
+  h->cfg.seed = seed;
+  h->sf.seed = seed;
+  h->sd.seed = seed;
+  int32_t* ep = h->cfg.precision == USV_F32 ? h->sf.episode : h->sd.episode;
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemset(ep, 0, (size_t)h->cfg.num_envs * 4));
+  return USV_OK;
+}
+
+int usv_reset(void* hp, const uint8_t* mask, float* obs, void* stream) {
+  Handle* h = as_handle(hp);
+  if (!h || !obs) return fail(USV_ERR_ARG, "null argument");
+  DeviceGuard g(h->device);
+  hipStream_t st = (hipStream_t)stream;
+  return h->cfg.precision == USV_F32 ? launch_reset<float>(h, h->sf, mask, obs, st)
+                                     : launch_reset<double>(h, h->sd, mask, obs, st);
+}
+
+int usv_step(void* hp, const float* act, float* obs, void* rew, uint8_t* term, uint8_t* trunc,
+             float* fobs, void* stream) {
+  Handle* h = as_handle(hp);
+  if (!h || !act || !obs || !rew || !term || !trunc) return fail(USV_ERR_ARG, "null argument");
+  DeviceGuard g(h->device);
+  hipStream_t st = (hipStream_t)stream;
+  return h->cfg.precision == USV_F32 ? launch_step<float>(h, h->sf, act, obs, rew, term, trunc, fobs, st)
+                                     : launch_step<double>(h, h->sd, act, obs, rew, term, trunc, fobs, st);
+}
+
+int usv_field_info(void* hp, int32_t f, int32_t* per_env, int32_t* is_int, const char** name) {
+  Handle* h = as_handle(hp);
+  if (!h || f < 0 || f >= USV_FIELD_COUNT) return fail(USV_ERR_ARG, "bad handle or field");
+  if (per_env) *per_env = field_per_env(h, f);
+  if (is_int) *is_int = kFields[f].is_int;
+  if (name) *name = kFields[f].name;
+  return USV_OK;
+}
+
+int usv_get_field(void* hp, int32_t f, void* host, size_t bytes) {
+  Handle* h = as_handle(hp);
+  if (!h || !host || f < 0 || f >= USV_FIELD_COUNT) return fail(USV_ERR_ARG, "bad argument");
+  if (bytes != field_bytes(h, f)) return fail(USV_ERR_ARG, "byte count mismatch");
+  DeviceGuard g(h->device);
+  return h->cfg.precision == USV_F32 ? field_io<float>(h, h->sf, f, host, true)
+                                     : field_io<double>(h, h->sd, f, host, true);
+}
+
+int usv_set_field(void* hp, int32_t f, const void* host, size_t bytes) {
+  Handle* h = as_handle(hp);
+  if (!h || !host || f < 0 || f >= USV_FIELD_COUNT) return fail(USV_ERR_ARG, "bad argument");
+  if (bytes != field_bytes(h, f)) return fail(USV_ERR_ARG, "byte count mismatch");
+  DeviceGuard g(h->device);
+  return h->cfg.precision == USV_F32 ? field_io<float>(h, h->sf, f, (void*)host, false)
+                                     : field_io<double>(h, h->sd, f, (void*)host, false);
+}
+
+size_t usv_state_bytes(void* hp) {
+  Handle* h = as_handle(hp);
+  if (!h) return 0;
+  size_t b = 0;
+  for (int f = 0; f < USV_FIELD_COUNT; ++f) b += field_bytes(h, f);
+  return b;
+}
+
+int usv_get_state(void* hp, void* host, size_t bytes) {
+  Handle* h = as_handle(hp);
+  if (!h || !host) return fail(USV_ERR_ARG, "bad argument");
+  if (bytes != usv_state_bytes(hp)) return fail(USV_ERR_ARG, "byte count mismatch");
+  char* p = (char*)host;
+  for (int f = 0; f < USV_FIELD_COUNT; ++f) {
+    const size_t fb = field_bytes(h, f);
+    const int rc = usv_get_field(hp, f, p, fb);
+    if (rc != USV_OK) return rc;
+    p += fb;
+  }
+  return USV_OK;
+}
+
+int usv_set_state(void* hp, const void* host, size_t bytes) {
+  Handle* h = as_handle(hp);
+  if (!h || !host) return fail(USV_ERR_ARG, "bad argument");
+  if (bytes != usv_state_bytes(hp)) return fail(USV_ERR_ARG, "byte count mismatch");
+  const char* p = (const char*)host;
+  for (int f = 0; f < USV_FIELD_COUNT; ++f) {
+    const size_t fb = field_bytes(h, f);
+    const int rc = usv_set_field(hp, f, p, fb);
+    if (rc != USV_OK) return rc;
+    p += fb;
+  }
+  return USV_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,28 @@
+"""gym_usv_amd — MI355X-native batched USV path-following environment.
+
+Registry mirroring gym_usv/__init__.py:3-39 for the ids on the accelerated path:
+
+    make("usv-simple")                         -> UsvSimpleEnv with TimeLimit(500)
+    make("usv-asmc-simple")                    -> UsvSimpleASMCEnv with TimeLimit(1000)
+    make_vec("usv-simple", num_envs=65536)     -> UsvVectorEnv (one HIP launch per step)
+
+The compute lives in libusvhip.so (HIP, gfx950) behind the C-ABI in include/usv_hip.h.
+"""
+from ._lib import UsvLibError, load as load_library  # noqa: F401
+from .vector_env import ENV_SPECS, UsvVectorEnv  # noqa: F401
+
+__all__ = ["make", "make_vec", "registry", "UsvVectorEnv", "UsvLibError", "ENV_SPECS"]
+
+registry = {k: {"entry_point": f"gym_usv_amd.envs:{cls}", "max_episode_steps": v[1]}
+            for (k, v), cls in zip(ENV_SPECS.items(), ("UsvSimpleEnv", "UsvSimpleASMCEnv"))}
+
+
+def make(env_id, max_episode_steps=None, **kwargs):
+    from . import envs
+    cls = {"usv-simple": envs.UsvSimpleEnv, "usv-asmc-simple": envs.UsvSimpleASMCEnv}[env_id]
+    limit = registry[env_id]["max_episode_steps"] if max_episode_steps is None else max_episode_steps
+    return cls(max_episode_steps=limit, **kwargs)
+
+
+def make_vec(env_id, num_envs, **kwargs):
+    return UsvVectorEnv(env_id, num_envs=num_envs, **kwargs)

@@ -1,0 +1,86 @@
+"""ctypes binding of libusvhip.so (C-ABI declared in include/usv_hip.h).
+
+The library is built in-tree (``__graft_entry__.build()`` / ``python -m gym_usv_amd.build``)
+and loaded from this package directory.  There is no fallback: if the HIP library is missing
+or fails to load, every env constructor raises ``UsvLibError``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+LIB_NAME = "libusvhip.so"
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+
+ABI_VERSION = 1
+MODE_SIMPLE, MODE_ASMC_SIMPLE = 0, 1
+F32, F64 = 0, 1
+AUTORESET_SAME_STEP, AUTORESET_DISABLED = 0, 1
+LIDAR_BRUTE, LIDAR_WINDOW = 0, 1
+OBS_DIM, SENSOR_COUNT, ACT_DIM, ASMC_STATE = 143, 128, 2, 16
+
+
+class UsvLibError(RuntimeError):
+    pass
+
+
+class UsvConfig(ctypes.Structure):
+    _fields_ = [("abi_version", ctypes.c_int32), ("mode", ctypes.c_int32),
+                ("precision", ctypes.c_int32), ("num_envs", ctypes.c_int32),
+                ("obstacle_cap", ctypes.c_int32), ("max_episode_steps", ctypes.c_int32),
+                ("autoreset", ctypes.c_int32), ("lidar_algo", ctypes.c_int32),
+                ("seed", ctypes.c_uint64), ("env_id_offset", ctypes.c_uint64)]
+
+
+# (name, restype, argtypes) for every function in include/usv_hip.h
+_vp, _i32, _u64, _sz = ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint64, ctypes.c_size_t
+SIGNATURES = [
+    ("usv_abi_version", ctypes.c_int, []),
+    ("usv_last_error", ctypes.c_char_p, []),
+    ("usv_config_default", None, [ctypes.POINTER(UsvConfig), _i32, _i32]),
+    ("usv_create", ctypes.c_int, [ctypes.POINTER(UsvConfig), _i32, ctypes.POINTER(_vp)]),
+    ("usv_destroy", None, [_vp]),
+    ("usv_num_envs", ctypes.c_int, [_vp]),
+    ("usv_obs_dim", ctypes.c_int, [_vp]),
+    ("usv_reward_bytes", ctypes.c_int, [_vp]),
+    ("usv_seed", ctypes.c_int, [_vp, _u64]),
+    ("usv_reset", ctypes.c_int, [_vp, _vp, _vp, _vp]),
+    ("usv_step", ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    ("usv_field_info", ctypes.c_int, [_vp, _i32, ctypes.POINTER(_i32), ctypes.POINTER(_i32),
+                                      ctypes.POINTER(ctypes.c_char_p)]),
+    ("usv_get_field", ctypes.c_int, [_vp, _i32, _vp, _sz]),
+    ("usv_set_field", ctypes.c_int, [_vp, _i32, _vp, _sz]),
+    ("usv_state_bytes", _sz, [_vp]),
+    ("usv_get_state", ctypes.c_int, [_vp, _vp, _sz]),
+    ("usv_set_state", ctypes.c_int, [_vp, _vp, _sz]),
+]
+
+_LIB = None
+
+
+def load():
+    """Load (once) and return the HIP library; raise UsvLibError if it is unavailable."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise UsvLibError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    try:
+        lib = ctypes.CDLL(LIB_PATH)
+    except OSError as e:  # pragma: no cover
+        raise UsvLibError(f"cannot load {LIB_PATH}: {e}") from e
+    for name, res, args in SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.usv_abi_version() != ABI_VERSION:
+        raise UsvLibError("libusvhip ABI version mismatch")
+    _LIB = lib
+    return lib
+
+
+def check(rc):
+    if rc != 0:
+        msg = load().usv_last_error().decode(errors="replace")
+        raise UsvLibError(f"libusvhip error {rc}: {msg}")
+    return rc

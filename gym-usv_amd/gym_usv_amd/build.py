@@ -1,0 +1,50 @@
+"""Build libusvhip.so in-tree for gfx950 (hipcc; no JIT cache, so the .so travels with the repo).
+
+    python -m gym_usv_amd.build        (from gym-usv_amd/, or via __graft_entry__.build())
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(PKG))
+CSRC = os.path.join(os.path.dirname(PKG), "csrc")
+INCLUDE = os.path.join(ROOT, "include")
+ARCH = os.environ.get("USV_OFFLOAD_ARCH", "gfx950")
+
+
+def hipcc():
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
+        if c and (os.path.isabs(c) and os.path.exists(c) or not os.path.isabs(c)):
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def sources():
+    return [os.path.join(CSRC, "usv_kernels.hip")]
+
+
+def deps():
+    return sources() + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hpp", ".h"))] + \
+        [os.path.join(INCLUDE, "usv_hip.h")]
+
+
+def build_library(force=False, verbose=True):
+    out = os.path.join(PKG, "libusvhip.so")
+    if not force and os.path.exists(out):
+        mt = os.path.getmtime(out)
+        if all(os.path.getmtime(d) <= mt for d in deps()):
+            return out
+    cmd = [hipcc(), "-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-shared", "-Wall",
+           f"-I{INCLUDE}", "-o", out + ".tmp"] + sources()
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    os.replace(out + ".tmp", out)
+    return out
+
+
+if __name__ == "__main__":
+    build_library(force="--force" in sys.argv)

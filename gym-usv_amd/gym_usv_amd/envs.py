@@ -1,0 +1,60 @@
+"""Single-env classes with the reference's Gymnasium ``Env`` API, backed by the HIP library.
+
+``UsvSimpleEnv`` / ``UsvSimpleASMCEnv`` keep the reference names and call signatures
+(gym_usv/envs/simple_env.py:7, simple_env_asmc.py:7): ``reset(seed=None, options=None) ->
+(obs float32[143], info)`` and ``step(action) -> (obs, reward, terminated, truncated, info)``
+with NumPy in/out.  Each is a 1-env ``UsvVectorEnv`` with autoreset off and no TimeLimit
+(``gym_usv_amd.make`` adds the registered TimeLimit, like ``gymnasium.make``).  They exist for
+API compatibility and debugging; throughput lives in ``UsvVectorEnv``.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from .vector_env import UsvVectorEnv
+
+
+class _SingleEnv:
+    env_id = None
+    metadata = {"render_modes": [], "render_fps": 30}
+
+    def __init__(self, render_mode=None, options=None, device=0, precision="f32",
+                 max_episode_steps=0, seed=None):
+        if render_mode not in (None,):
+            raise NotImplementedError("rendering is out of scope (SURVEY.md §2 #13)")
+        self.render_mode = render_mode
+        self.options = options or {}
+        self._venv = UsvVectorEnv(self.env_id, num_envs=1, device=device, precision=precision,
+                                  autoreset=False, max_episode_steps=max_episode_steps,
+                                  seed=0 if seed is None else seed)
+        self.observation_space = self._venv.single_observation_space
+        self.action_space = self._venv.single_action_space
+        self._seeded = False
+
+    def reset(self, seed=None, options=None):
+        if seed is None and not self._seeded:
+            seed = int(np.random.SeedSequence().entropy % (1 << 63))
+        if seed is not None:
+            self._seeded = True
+        obs, _ = self._venv.reset(seed=seed, options=options)
+        return obs[0].cpu().numpy(), {}
+
+    def step(self, action):
+        a = torch.as_tensor(np.asarray(action, dtype=np.float32).reshape(1, 2), device=self._venv.device)
+        obs, rew, term, trunc, _ = self._venv.step(a)
+        return (obs[0].cpu().numpy(), float(rew[0].item()), bool(term[0].item()),
+                bool(trunc[0].item()), {})
+
+    def close(self):
+        self._venv.close()
+
+
+class UsvSimpleEnv(_SingleEnv):
+    """HIP-backed ``UsvSimpleEnv`` (id usv-simple)."""
+    env_id = "usv-simple"
+
+
+class UsvSimpleASMCEnv(_SingleEnv):
+    """HIP-backed ``UsvSimpleASMCEnv`` (id usv-asmc-simple)."""
+    env_id = "usv-asmc-simple"

@@ -1,0 +1,176 @@
+"""Batched HIP vector env: the gymnasium ``VectorEnv`` reset()/step() surface over libusvhip.
+
+Replaces N x ``UsvSimpleEnv`` / ``UsvSimpleASMCEnv`` (gym_usv/envs/simple_env.py:7-349,
+simple_env_asmc.py:7-32) stepped one by one by SB3's DummyVecEnv
+(train_test/sb3_train_vec.py:67): one kernel launch steps every env, outputs stay in HBM as
+torch tensors, done envs are reset inside the same launch (same-step autoreset, the terminal
+observation in ``info["final_obs"]``), and the TimeLimit of the registered id
+(gym_usv/__init__.py:24-34) is applied in-kernel.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from .spaces import Box
+
+ENV_SPECS = {
+    # id: (mode, max_episode_steps)  -- gym_usv/__init__.py:24-34
+    "usv-simple": (_lib.MODE_SIMPLE, 500),
+    "usv-asmc-simple": (_lib.MODE_ASMC_SIMPLE, 1000),
+}
+
+
+def _stream_ptr(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+class UsvVectorEnv:
+    """``num_envs`` USV path-following envs on one GPU.
+
+    reset(seed=None, options=None, mask=None) -> (obs [N,143] f32, info)
+    step(actions [N,2] f32)  -> (obs, reward [N], terminated [N] bool, truncated [N] bool, info)
+
+    Returned tensors are the env's own device buffers (zero-copy); they are overwritten by the
+    next call — clone them to keep them.  ``info["final_obs"]`` holds the terminal obs rows of
+    envs that ended this step (``info["_final_obs"]`` is the mask).
+    """
+
+    metadata = {"render_modes": [], "autoreset_mode": "same-step"}
+
+    def __init__(self, env_id="usv-simple", num_envs=4096, device=0, seed=0, precision="f32",
+                 autoreset=True, max_episode_steps=None, obstacle_cap=32, lidar="brute",
+                 env_id_offset=0):
+        if env_id not in ENV_SPECS:
+            raise ValueError(f"unknown env id {env_id!r}; known: {sorted(ENV_SPECS)}")
+        if not torch.cuda.is_available():
+            raise _lib.UsvLibError("UsvVectorEnv needs a ROCm GPU (torch.cuda.is_available() is False)")
+        self.lib = _lib.load()
+        mode, limit = ENV_SPECS[env_id]
+        self.env_id, self.num_envs = env_id, int(num_envs)
+        self.device = torch.device("cuda", device)
+        cfg = _lib.UsvConfig()
+        self.lib.usv_config_default(ctypes.byref(cfg), mode, self.num_envs)
+        cfg.precision = {"f32": _lib.F32, "f64": _lib.F64}[precision]
+        cfg.obstacle_cap = obstacle_cap
+        cfg.max_episode_steps = limit if max_episode_steps is None else int(max_episode_steps)
+        cfg.autoreset = _lib.AUTORESET_SAME_STEP if autoreset else _lib.AUTORESET_DISABLED
+        cfg.lidar_algo = {"brute": _lib.LIDAR_BRUTE, "window": _lib.LIDAR_WINDOW}[lidar]
+        cfg.seed = int(seed)
+        cfg.env_id_offset = int(env_id_offset)
+        self.cfg = cfg
+        h = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            _lib.check(self.lib.usv_create(ctypes.byref(cfg), self.device.index, ctypes.byref(h)))
+        self._h = h
+        n = self.num_envs
+        rdt = torch.float32 if precision == "f32" else torch.float64
+        kw = dict(device=self.device)
+        self.obs = torch.zeros((n, _lib.OBS_DIM), dtype=torch.float32, **kw)
+        self.final_obs = torch.zeros((n, _lib.OBS_DIM), dtype=torch.float32, **kw)
+        self.reward = torch.zeros(n, dtype=rdt, **kw)
+        self._term = torch.zeros(n, dtype=torch.uint8, **kw)
+        self._trunc = torch.zeros(n, dtype=torch.uint8, **kw)
+        self.max_episode_steps = cfg.max_episode_steps
+        # spaces (simple_env.py:27,30)
+        self.single_observation_space = Box(-1, 1, shape=(_lib.OBS_DIM,), dtype=np.float32)
+        self.single_action_space = Box(np.array([0.2, -1]), np.array([1, 1]), shape=(2,), dtype=np.float32)
+        self._fields = self._field_table()
+
+    # ------------------------------------------------------------------ API
+    def reset(self, seed=None, options=None, mask=None):
+        if options:
+            raise NotImplementedError("reset options (place_obstacles_on_path) are not supported yet")
+        if seed is not None:
+            _lib.check(self.lib.usv_seed(self._h, ctypes.c_uint64(int(seed))))
+        m = None
+        if mask is not None:
+            m = torch.as_tensor(mask, device=self.device).to(torch.uint8).contiguous()
+        _lib.check(self.lib.usv_reset(self._h, _ptr(m), _ptr(self.obs), _stream_ptr(self.device)))
+        return self.obs, {}
+
+    def step(self, actions):
+        a = torch.as_tensor(actions, device=self.device)
+        if a.dtype != torch.float32 or not a.is_contiguous():
+            a = a.to(torch.float32).contiguous()
+        if a.shape != (self.num_envs, _lib.ACT_DIM):
+            raise ValueError(f"actions must be [{self.num_envs}, 2], got {tuple(a.shape)}")
+        _lib.check(self.lib.usv_step(self._h, _ptr(a), _ptr(self.obs), _ptr(self.reward),
+                                     _ptr(self._term), _ptr(self._trunc), _ptr(self.final_obs),
+                                     _stream_ptr(self.device)))
+        term = self._term.view(torch.bool)
+        trunc = self._trunc.view(torch.bool)
+        info = {"final_obs": self.final_obs, "_final_obs": term | trunc}
+        return self.obs, self.reward, term, trunc, info
+
+    def step_raw(self, actions, obs, reward, term, trunc, final_obs=None, stream=None):
+        """Launch one step into caller-owned buffers (no checks, no allocation): bench / graphs."""
+        st = ctypes.c_void_p(stream) if stream is not None else _stream_ptr(self.device)
+        return self.lib.usv_step(self._h, _ptr(actions), _ptr(obs), _ptr(reward), _ptr(term),
+                                 _ptr(trunc), _ptr(final_obs), st)
+
+    # ------------------------------------------------------------------ state exchange
+    def _field_table(self):
+        tab = {}
+        per, isint, name = ctypes.c_int32(), ctypes.c_int32(), ctypes.c_char_p()
+        for f in range(64):
+            if self.lib.usv_field_info(self._h, f, ctypes.byref(per), ctypes.byref(isint),
+                                       ctypes.byref(name)) != 0:
+                break
+            tab[name.value.decode()] = (f, per.value, bool(isint.value))
+        return tab
+
+    @property
+    def field_names(self):
+        return list(self._fields)
+
+    def get_field(self, name):
+        f, per, isint = self._fields[name]
+        shape = (self.num_envs,) if per == 1 else (self.num_envs, per)
+        out = np.zeros(shape, dtype=np.int32 if isint else np.float64)
+        _lib.check(self.lib.usv_get_field(self._h, f, out.ctypes.data_as(ctypes.c_void_p), out.nbytes))
+        return out
+
+    def set_field(self, name, value):
+        f, per, isint = self._fields[name]
+        shape = (self.num_envs,) if per == 1 else (self.num_envs, per)
+        arr = np.ascontiguousarray(np.broadcast_to(np.asarray(value), shape),
+                                   dtype=np.int32 if isint else np.float64)
+        _lib.check(self.lib.usv_set_field(self._h, f, arr.ctypes.data_as(ctypes.c_void_p), arr.nbytes))
+
+    def get_state(self):
+        """All per-env state as {field: ndarray} (env checkpoint / parity inspection)."""
+        return {k: self.get_field(k) for k in self._fields}
+
+    def set_state(self, state):
+        for k, v in state.items():
+            self.set_field(k, v)
+
+    def state_blob(self):
+        n = self.lib.usv_state_bytes(self._h)
+        buf = np.zeros(n, dtype=np.uint8)
+        _lib.check(self.lib.usv_get_state(self._h, buf.ctypes.data_as(ctypes.c_void_p), n))
+        return buf
+
+    def load_state_blob(self, blob):
+        blob = np.ascontiguousarray(blob, dtype=np.uint8)
+        _lib.check(self.lib.usv_set_state(self._h, blob.ctypes.data_as(ctypes.c_void_p), blob.nbytes))
+
+    def close(self):
+        if getattr(self, "_h", None):
+            torch.cuda.synchronize(self.device)
+            self.lib.usv_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,155 @@
+/*
+ * usv_hip.h — C-ABI of libusvhip.so, the MI355X-native batched USV path-following
+ * environment (usv-simple / usv-asmc-simple step on gfx950).
+ *
+ * Drop-in boundary.  The reference (romi2002/gym-usv) is pure Python; its interface for
+ * this path is the Gymnasium Env API of its env classes, driven N-at-a-time by SB3's
+ * DummyVecEnv (train_test/sb3_train_vec.py:67).  Each entry point below replaces:
+ *
+ *   usv_create      <- gymnasium.make(env_id) x N / UsvSimpleEnv.__init__
+ *                      (gym_usv/__init__.py:24-34, gym_usv/envs/simple_env.py:10-60,
+ *                       gym_usv/envs/simple_env_asmc.py:10-12)
+ *   usv_seed        <- Env.reset(seed=...) seeding of np_random (simple_env.py:229)
+ *   usv_reset       <- UsvSimpleEnv.reset (simple_env.py:228-308),
+ *                      UsvSimpleASMCEnv.reset (simple_env_asmc.py:14-16)
+ *   usv_step        <- UsvSimpleEnv.step (simple_env.py:310-346),
+ *                      UsvSimpleASMCEnv.step (simple_env_asmc.py:18-27) -> UsvAsmc.compute
+ *                      (gym_usv/control/usv_asmc.py:53-244), lidar
+ *                      (gym_usv/envs/usv_asmc_ca_env.py:411-461,500-519), TimeLimit
+ *                      (gym_usv/__init__.py:27,33) and DummyVecEnv same-step autoreset
+ *   usv_get_field / usv_set_field / usv_get_state / usv_set_state
+ *                   <- the env attributes (position, velocity, obstacle_positions, ...);
+ *                      used for checkpointing and for parity state injection
+ *
+ * Conventions: plain pointers and sizes, no torch / HIP types.  `stream` is a hipStream_t
+ * passed as void* (NULL = default stream).  Device pointers (`*_dev`) are caller-owned
+ * device memory (e.g. torch tensors' data_ptr()).  Launches are asynchronous and
+ * stream-ordered.  Every function returns 0 on success or a negative usv_status; the
+ * message is in usv_last_error() (thread-local).  A handle is not thread-safe; use one
+ * handle per device (one process per GPU).
+ */
+#ifndef USV_HIP_H
+#define USV_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define USV_ABI_VERSION 1
+#define USV_SENSOR_COUNT 128
+#define USV_OBS_DIM 143      /* 15 + 128, simple_env.py:27 */
+#define USV_ACT_DIM 2        /* simple_env.py:30 */
+#define USV_ASMC_STATE 16    /* unique UsvAsmc state values (usv_asmc.py:43-49) */
+
+typedef enum usv_status {
+  USV_OK = 0,
+  USV_ERR_ARG = -1,
+  USV_ERR_HIP = -2,
+  USV_ERR_ABI = -3,
+  USV_ERR_STATE = -4
+} usv_status;
+
+typedef enum usv_mode {
+  USV_MODE_SIMPLE = 0,       /* id "usv-simple"      (UsvSimpleEnv)      */
+  USV_MODE_ASMC_SIMPLE = 1   /* id "usv-asmc-simple" (UsvSimpleASMCEnv)  */
+} usv_mode;
+
+typedef enum usv_precision { USV_F32 = 0, USV_F64 = 1 } usv_precision;
+
+typedef enum usv_autoreset {
+  USV_AUTORESET_SAME_STEP = 0, /* done envs reset inside usv_step (SB3 DummyVecEnv) */
+  USV_AUTORESET_DISABLED = 1   /* done envs keep stepping until usv_reset(mask)       */
+} usv_autoreset;
+
+typedef enum usv_lidar_algo {
+  USV_LIDAR_BRUTE = 0,  /* every (ray, obstacle) pair                         */
+  USV_LIDAR_WINDOW = 1  /* angular-window pruning, bit-identical to BRUTE    */
+} usv_lidar_algo;
+
+typedef struct usv_config {
+  int32_t abi_version;       /* must be USV_ABI_VERSION */
+  int32_t mode;              /* usv_mode */
+  int32_t precision;         /* usv_precision: state + arithmetic type; obs is always f32 */
+  int32_t num_envs;          /* envs owned by this handle */
+  int32_t obstacle_cap;      /* max obstacles per env (reference draws 15..29) */
+  int32_t max_episode_steps; /* TimeLimit; 0 = none. 500 usv-simple, 1000 usv-asmc-simple */
+  int32_t autoreset;         /* usv_autoreset */
+  int32_t lidar_algo;        /* usv_lidar_algo */
+  uint64_t seed;             /* Philox key for in-kernel resets */
+  uint64_t env_id_offset;    /* global id of env 0 (sharding across GPUs) */
+} usv_config;
+
+/* Per-env state fields.  Host-side layout for get/set: [num_envs][per_env] row-major,
+ * float64 for real fields, int32 for integer fields (usv_field_info tells which). */
+typedef enum usv_field {
+  USV_FIELD_X = 0, USV_FIELD_Y, USV_FIELD_PSI,          /* position (simple_env.py:39) */
+  USV_FIELD_U, USV_FIELD_V, USV_FIELD_R,                /* velocity (:38)              */
+  USV_FIELD_LAST_U, USV_FIELD_LAST_R,                   /* last_action[0], [2] (:41)   */
+  USV_FIELD_PROGRESS,                                   /* progress (:53)              */
+  USV_FIELD_PATH_X0, USV_FIELD_PATH_Y0,                 /* path_start (:51)            */
+  USV_FIELD_PATH_X1, USV_FIELD_PATH_Y1,                 /* path_end (:52)              */
+  USV_FIELD_MAX_U, USV_FIELD_MAX_R,                     /* max_action[0], [2] (:32)    */
+  USV_FIELD_REF_V,                                      /* reference_velocity (:33)    */
+  USV_FIELD_N_OBS,          /* int: obstacle_n (:44)                                    */
+  USV_FIELD_ELAPSED,        /* int: TimeLimit elapsed steps                              */
+  USV_FIELD_EPISODE,        /* int: episode counter (Philox counter word)                */
+  USV_FIELD_SCAN_VALID,     /* int: 1 if the current pose's scan is the stale sensor_data */
+  USV_FIELD_OBS_X, USV_FIELD_OBS_Y, USV_FIELD_OBS_R,    /* [cap] obstacles (:45-46)    */
+  USV_FIELD_SENSOR_LAST,    /* [128] stale scan for reset obs (sensor_data, :47)          */
+  USV_FIELD_ASMC,           /* [16] UsvAsmc state (usv-asmc-simple only)                  */
+  USV_FIELD_COUNT
+} usv_field;
+
+int usv_abi_version(void);
+const char* usv_last_error(void);
+
+/* Fill `cfg` with the reference defaults for `mode` (cap 32, TimeLimit by id, f32,
+ * same-step autoreset, window lidar, seed 0). */
+void usv_config_default(usv_config* cfg, int32_t mode, int32_t num_envs);
+
+int usv_create(const usv_config* cfg, int32_t device, void** handle_out);
+void usv_destroy(void* handle);
+
+int usv_num_envs(void* handle);
+int usv_obs_dim(void* handle);
+/* Bytes of one reward element (4 for USV_F32, 8 for USV_F64). */
+int usv_reward_bytes(void* handle);
+
+/* Re-key the reset RNG (Philox4x32-10, key = seed, counter = global env id / episode)
+ * and zero every episode counter.  Host-side only; no launch. */
+int usv_seed(void* handle, uint64_t seed);
+
+/* Reset envs whose mask byte is non-zero (all envs if mask_dev == NULL) and write their
+ * reset observation rows into obs_dev [num_envs][obs_dim] (other rows untouched). */
+int usv_reset(void* handle, const uint8_t* mask_dev, float* obs_dev, void* stream);
+
+/* One env step for every env.
+ *   act_dev       [num_envs][2] f32   (u in [0.2,1], r in [-1,1]; usv-asmc-simple: (u_d, psi offset))
+ *   obs_dev       [num_envs][obs_dim] f32  (reset obs for envs that autoreset)
+ *   rew_dev       [num_envs] f32 or f64 (usv_reward_bytes)
+ *   term_dev, trunc_dev [num_envs] u8
+ *   final_obs_dev [num_envs][obs_dim] f32 or NULL: terminal obs rows of done envs
+ *                 (rows of envs not done are left untouched). */
+int usv_step(void* handle, const float* act_dev, float* obs_dev, void* rew_dev,
+             uint8_t* term_dev, uint8_t* trunc_dev, float* final_obs_dev, void* stream);
+
+/* Field metadata: values per env, 1 if int32, name. */
+int usv_field_info(void* handle, int32_t field, int32_t* per_env, int32_t* is_int,
+                   const char** name);
+/* Synchronous host copies (device synchronised first). `bytes` must equal
+ * num_envs * per_env * (is_int ? 4 : 8). */
+int usv_get_field(void* handle, int32_t field, void* host, size_t bytes);
+int usv_set_field(void* handle, int32_t field, const void* host, size_t bytes);
+
+/* Whole-state blob (all fields in enum order, host layout as above): env checkpoint. */
+size_t usv_state_bytes(void* handle);
+int usv_get_state(void* handle, void* host, size_t bytes);
+int usv_set_state(void* handle, const void* host, size_t bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* USV_HIP_H */

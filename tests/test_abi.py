@@ -1,0 +1,73 @@
+"""C-ABI checks that need no GPU: the library builds/loads, exports every function declared in
+include/usv_hip.h, and reports errors through its return codes instead of crashing."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import ROOT
+
+
+def _declared_functions():
+    src = open(os.path.join(ROOT, "include", "usv_hip.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?\w+\**\s+\**(usv_\w+)\s*\(", src, flags=re.M)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from gym_usv_amd import _lib
+    from gym_usv_amd.build import build_library
+    build_library(verbose=False)
+    return _lib.load()
+
+
+def test_header_declares_full_api():
+    names = _declared_functions()
+    assert {"usv_create", "usv_step", "usv_reset", "usv_get_state", "usv_set_state",
+            "usv_last_error", "usv_abi_version"} <= set(names)
+
+
+def test_every_declared_symbol_exported(lib):
+    from gym_usv_amd import _lib
+    bound = {n for n, _, _ in _lib.SIGNATURES}
+    for name in _declared_functions():
+        assert hasattr(lib, name), f"{name} declared in usv_hip.h but not exported"
+        assert name in bound, f"{name} declared in usv_hip.h but not bound in _lib.py"
+
+
+def test_abi_version_and_defaults(lib):
+    from gym_usv_amd import _lib
+    assert lib.usv_abi_version() == _lib.ABI_VERSION
+    cfg = _lib.UsvConfig()
+    lib.usv_config_default(ctypes.byref(cfg), _lib.MODE_SIMPLE, 128)
+    assert (cfg.abi_version, cfg.num_envs, cfg.obstacle_cap, cfg.max_episode_steps) == (1, 128, 32, 500)
+    lib.usv_config_default(ctypes.byref(cfg), _lib.MODE_ASMC_SIMPLE, 8)
+    assert cfg.max_episode_steps == 1000          # gym_usv/__init__.py:33
+
+
+def test_create_rejects_bad_config_without_gpu(lib):
+    from gym_usv_amd import _lib
+    cfg = _lib.UsvConfig()
+    lib.usv_config_default(ctypes.byref(cfg), _lib.MODE_SIMPLE, 16)
+    h = ctypes.c_void_p()
+    cfg.obstacle_cap = 8                           # reference draws up to 29 obstacles
+    assert lib.usv_create(ctypes.byref(cfg), 0, ctypes.byref(h)) != 0
+    assert b"obstacle_cap" in lib.usv_last_error()
+    cfg.obstacle_cap = 32
+    cfg.abi_version = 99
+    assert lib.usv_create(ctypes.byref(cfg), 0, ctypes.byref(h)) == -3
+    assert not h.value
+    # null handles are reported, not dereferenced
+    assert lib.usv_step(None, None, None, None, None, None, None, None) == -1
+    assert lib.usv_reset(None, None, None, None) == -1
+
+
+def test_vector_env_fails_loudly_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    import gym_usv_amd
+    with pytest.raises(gym_usv_amd.UsvLibError):
+        gym_usv_amd.make_vec("usv-simple", 8)
