@@ -72,6 +72,8 @@ __device__ __forceinline__ float  m_exp(float x)  { return expf(x); }
 __device__ __forceinline__ double m_exp(double x) { return exp(x); }
 __device__ __forceinline__ float  m_hypot(float x, float y)  { return hypotf(x, y); }
 __device__ __forceinline__ double m_hypot(double x, double y) { return hypot(x, y); }
+__device__ __forceinline__ float  m_fma(float a, float b, float c)  { return fmaf(a, b, c); }
+__device__ __forceinline__ double m_fma(double a, double b, double c) { return fma(a, b, c); }
 __device__ __forceinline__ float  m_abs(float x)  { return fabsf(x); }
 __device__ __forceinline__ double m_abs(double x) { return fabs(x); }
 
@@ -104,13 +106,39 @@ __device__ __forceinline__ double bcast(double v, int lane) {
   const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
   return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
+__device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// DPP lane moves (gfx9 dpp_ctrl encodings): quad_perm [1,0,3,2], [2,3,0,1],
+// row_half_mirror, row_mirror.  Inactive/out-of-row sources keep `v` (bound_ctrl off).
+template <int CTRL> __device__ __forceinline__ float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL> __device__ __forceinline__ double dpp(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp((int)(b & 0xffffffffll), (int)(b & 0xffffffffll), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp((int)(b >> 32), (int)(b >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+constexpr int kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppHalfMirror = 0x141, kDppMirror = 0x140;
+
+template <typename T> __device__ __forceinline__ T tmin(T a, T b) { return b < a ? b : a; }
+template <typename T> __device__ __forceinline__ T tmax(T a, T b) { return b > a ? b : a; }
+
+// Wave-wide min / max, result wave-uniform: 4 DPP steps reduce each 16-lane row, then the
+// four row results are combined through v_readlane (no LDS round trips).
 template <typename T> __device__ __forceinline__ T wave_min(T v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    const T o = __shfl_xor(v, off, kWave);
-    v = o < v ? o : v;
-  }
-  return v;
+  v = tmin(v, dpp<kDppXor1>(v));
+  v = tmin(v, dpp<kDppXor2>(v));
+  v = tmin(v, dpp<kDppHalfMirror>(v));
+  v = tmin(v, dpp<kDppMirror>(v));
+  return tmin(tmin(bcast(v, 0), bcast(v, 16)), tmin(bcast(v, 32), bcast(v, 48)));
+}
+template <typename T> __device__ __forceinline__ T wave_max(T v) {
+  v = tmax(v, dpp<kDppXor1>(v));
+  v = tmax(v, dpp<kDppXor2>(v));
+  v = tmax(v, dpp<kDppHalfMirror>(v));
+  v = tmax(v, dpp<kDppMirror>(v));
+  return tmax(tmax(bcast(v, 0), bcast(v, 16)), tmax(bcast(v, 32), bcast(v, 48)));
 }
 
 // ----------------------------------------------------------------------------- Philox RNG

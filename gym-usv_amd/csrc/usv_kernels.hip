@@ -136,9 +136,10 @@ __device__ void reset_env(const State<R>& S, int e, float (&hdr)[kHdr]) {
 // --------------------------------------------------------------------------- phase 1
 // UsvSimpleEnv.step kinematics..reward terms (simple_env.py:310-346); for usv-asmc-simple
 // first 2x UsvAsmc.compute (simple_env_asmc.py:18-27) and then step(zeros(2)).
+// Also returns sin/cos of the new heading so the wave-per-env lidar does not recompute them.
 template <typename R, int MODE>
 __device__ void env_dynamics(const State<R>& S, int e, float a_u, float a_r, float (&hdr)[kHdr],
-                             R& px, R& py, R& ppsi, R& partial, bool& trunc) {
+                             R& px, R& py, R& psp, R& pcp, R& partial, bool& trunc) {
   R x = S.f[F_X][e], y = S.f[F_Y][e], psi = S.f[F_PSI][e];
   R u = S.f[F_U][e], v = S.f[F_V][e], r = S.f[F_R][e];
   if (MODE == USV_MODE_ASMC_SIMPLE) {
@@ -201,56 +202,80 @@ __device__ void env_dynamics(const State<R>& S, int e, float a_u, float a_r, flo
   S.f[F_PROGRESS][e] = a;
   S.elapsed[e] = el;
   S.scan_valid[e] = 1;
-  px = x; py = y; ppsi = psi;
+  px = x; py = y;
+  m_sincos(psi, &psp, &pcp);
 }
 
 // --------------------------------------------------------------------------- lidar
-// 128-ray lidar of env e at pose (px, py, psi), wave-per-env.  Lane l owns rays l, l+64.
-// Restates compute_sensor_measurments / compute_obstacle_positions /
-// _compute_sensor_distances (usv_asmc_ca_env.py:411-461, 500-519): per ray, the hit
-// obstacle with the smallest key d_j = |c_j - p| - r_j (== first hit in argsort order).
-template <typename R>
-__device__ __forceinline__ void ray_test(R c, R s, R jdx, R jdy, R jr2, R jk, R& bk, R& bp, R& bd) {
-  const R proj = jdx * c + jdy * s;        // obstacle x in the ray frame (:506-517)
-  const R perp = jdx * s - jdy * c;        // obstacle y, mirrored (:518)
-  const R delta = jr2 - perp * perp;       // :453
-  bool hit = (proj >= R(0)) & (delta >= R(0));
-  if (hit && !(proj < R(kSensorMax))) hit = (proj - m_sqrt(delta)) < R(kSensorMax);  // :458
-  if (hit & (jk < bk)) { bk = jk; bp = proj; bd = delta; }
+// 128-ray lidar of one env at pose (px, py, heading sin/cos), wave-per-env.  Lane l owns rays
+// l and l+64; lane j holds obstacle j (`o`, already loaded).  Restates
+// compute_sensor_measurments / compute_obstacle_positions / _compute_sensor_distances
+// (usv_asmc_ca_env.py:411-461, 500-519): per ray, the hit obstacle with the smallest key
+// d_j = |c_j - p| - r_j, which equals the reference's first hit in argsort(d) order.
+// Every product is an explicit fma or a rounded multiply, so the step and reset kernels
+// produce bit-identical scans (the stale-scan reset obs depends on it).
+template <typename R> struct Ray { R c, s, bk; int bj; };
+
+template <typename R, bool RANGE_CHECK>
+__device__ __forceinline__ void ray_pair(Ray<R>& ra, R jdx, R jdy, R jr2, R jk, int j) {
+  const R proj = m_fma(jdx, ra.c, jdy * ra.s);    // obstacle x in the ray frame (:506-517)
+  const R perp = m_fma(jdx, ra.s, -(jdy * ra.c)); // obstacle y, mirrored (:518)
+  const R delta = m_fma(-perp, perp, jr2);        // r^2 - y^2 (:453)
+  bool hit = (proj >= R(0)) & (delta >= R(0)) & (jk < ra.bk);
+  if (RANGE_CHECK) hit = hit && (proj - m_sqrt(delta)) < R(kSensorMax);   // :458
+  ra.bk = hit ? jk : ra.bk;
+  ra.bj = hit ? j : ra.bj;
+}
+
+template <typename R, bool RANGE_CHECK>
+__device__ __forceinline__ void ray_loop(Ray<R>& r0, Ray<R>& r1, R dx, R dy, R r2, R key, int n) {
+  for (int j = 0; j < n; ++j) {                  // n wave-uniform: scalar loop, v_readlane bcast
+    const R jdx = bcast(dx, j), jdy = bcast(dy, j), jr2 = bcast(r2, j), jk = bcast(key, j);
+    ray_pair<R, RANGE_CHECK>(r0, jdx, jdy, jr2, jk, j);
+    ray_pair<R, RANGE_CHECK>(r1, jdx, jdy, jr2, jk, j);
+  }
 }
 
 template <typename R>
-__device__ void lidar_wave(const State<R>& S, int e, int n, R px, R py, R psi, R co0, R so0,
-                           R co1, R so1, R& rd0, R& rd1, R& min_key) {
+__device__ __forceinline__ R ray_reading(const Ray<R>& ra, R dx, R dy, R r2) {
+  const int src = ra.bj < 0 ? 0 : ra.bj;
+  const R gdx = __shfl(dx, src, kWave), gdy = __shfl(dy, src, kWave), gr2 = __shfl(r2, src, kWave);
+  const R proj = m_fma(gdx, ra.c, gdy * ra.s);
+  const R perp = m_fma(gdx, ra.s, -(gdy * ra.c));
+  const R delta = m_fma(-perp, perp, gr2);
+  return ra.bj >= 0 ? proj - m_sqrt(delta) : R(kSensorMax);                     // :457-459
+}
+
+template <typename R>
+__device__ __forceinline__ void lidar_wave(const R4<R>& o, int n, R px, R py, R sp, R cp, R co0,
+                                           R so0, R co1, R so1, R& rd0, R& rd1, R& min_key) {
   const int l = lane_id();
-  R dx = R(0), dy = R(0), r2 = R(0), key = big<R>();
-  if (l < n) {                                                // lane j = obstacle j
-    const R4<R> o = S.obst[(size_t)e * S.cap + l];
-    dx = o.x - px;
-    dy = o.y - py;
-    r2 = o.w;
-    key = m_sqrt(dx * dx + dy * dy) - o.z;                    // simple_env.py:205-206
-  }
+  const bool valid = l < n;
+  const R dx = o.x - px, dy = o.y - py, r2 = o.w;
+  const R d = m_sqrt(m_fma(dx, dx, dy * dy));
+  const R key = valid ? d - o.z : big<R>();                 // simple_env.py:205-206
   min_key = wave_min(key);
-  R sp, cp;
-  m_sincos(psi, &sp, &cp);
-  // ray angle = psi + (start + i*res) (usv_asmc_ca_env.py:420-423), by rotation
-  const R c0 = cp * co0 - sp * so0, s0 = sp * co0 + cp * so0;
-  const R c1 = cp * co1 - sp * so1, s1 = sp * co1 + cp * so1;
-  R bk0 = big<R>(), bp0 = R(0), bd0 = R(0);
-  R bk1 = big<R>(), bp1 = R(0), bd1 = R(0);
-  for (int j = 0; j < n; ++j) {                               // wave-uniform obstacle loop
-    const R jdx = bcast(dx, j), jdy = bcast(dy, j), jr2 = bcast(r2, j), jk = bcast(key, j);
-    ray_test(c0, s0, jdx, jdy, jr2, jk, bk0, bp0, bd0);
-    ray_test(c1, s1, jdx, jdy, jr2, jk, bk1, bp1, bd1);
-  }
-  rd0 = bk0 < big<R>() ? bp0 - m_sqrt(bd0) : R(kSensorMax);   // :457-459, else max range
-  rd1 = bk1 < big<R>() ? bp1 - m_sqrt(bd1) : R(kSensorMax);
+  // ray angle psi + (start + i*res) (usv_asmc_ca_env.py:420-423) by rotating the offset table
+  Ray<R> r0{m_fma(cp, co0, -(sp * so0)), m_fma(sp, co0, cp * so0), big<R>(), -1};
+  Ray<R> r1{m_fma(cp, co1, -(sp * so1)), m_fma(sp, co1, cp * so1), big<R>(), -1};
+  // A reading is <= proj <= |c_j - p|; the reference's "< max range" test (:458) can only
+  // reject when some obstacle is ~100 m away, so it is evaluated only then (wave-uniform).
+  const R far = wave_max(valid ? d : R(0));
+  if (far < R(0.99 * kSensorMax)) ray_loop<R, false>(r0, r1, dx, dy, r2, key, n);
+  else ray_loop<R, true>(r0, r1, dx, dy, r2, key, n);
+  rd0 = ray_reading(r0, dx, dy, r2);
+  rd1 = ray_reading(r1, dx, dy, r2);
+}
+
+template <typename R>
+__device__ __forceinline__ R4<R> load_obstacle(const State<R>& S, int e, int l) {
+  return l < S.cap ? S.obst[(size_t)e * S.cap + l] : R4<R>{R(0), R(0), R(0), R(0)};
 }
 
 template <typename R> struct Scratch {
   float hdr[kHdr][kEPB + 1];
-  R px[kEPB], py[kEPB], psi[kEPB], partial[kEPB], msens[kEPB];
+  R px[kEPB], py[kEPB], sp[kEPB], cp[kEPB], partial[kEPB], msens[kEPB];
+  int n[kEPB];
   uint8_t trunc[kEPB], term[kEPB];
 };
 
@@ -262,33 +287,37 @@ __global__ __launch_bounds__(kBlock) void step_kernel(State<R> S, IO<R> io) {
   const int wave = tid / kWave;
   const int l = lane_id();
   const int e0 = blockIdx.x * kEPB;
+  const int ne = S.N - e0 < kEPB ? S.N - e0 : kEPB;   // envs of this block
+
+  // obstacle rows of this wave's first env: issued before phase 1 to overlap its latency
+  R4<R> o_next = wave < ne ? load_obstacle(S, e0 + wave, l) : R4<R>{};
 
   // ---- phase 1: lane-per-env dynamics
-  if (tid < kEPB) {
+  if (tid < ne) {
     const int e = e0 + tid;
-    if (e < S.N) {
-      const float2 a = reinterpret_cast<const float2*>(io.act)[e];
-      float hdr[kHdr];
-      R px, py, psi, partial;
-      bool trunc;
-      env_dynamics<R, MODE>(S, e, a.x, a.y, hdr, px, py, psi, partial, trunc);
+    const float2 a = reinterpret_cast<const float2*>(io.act)[e];
+    float hdr[kHdr];
+    R px, py, sp, cp, partial;
+    bool trunc;
+    env_dynamics<R, MODE>(S, e, a.x, a.y, hdr, px, py, sp, cp, partial, trunc);
 #pragma unroll
-      for (int i = 0; i < kHdr; ++i) sh.hdr[i][tid] = hdr[i];
-      sh.px[tid] = px; sh.py[tid] = py; sh.psi[tid] = psi;
-      sh.partial[tid] = partial;
-      sh.trunc[tid] = trunc;
-    }
+    for (int i = 0; i < kHdr; ++i) sh.hdr[i][tid] = hdr[i];
+    sh.px[tid] = px; sh.py[tid] = py; sh.sp[tid] = sp; sh.cp[tid] = cp;
+    sh.partial[tid] = partial;
+    sh.trunc[tid] = trunc;
+    sh.n[tid] = S.n_obs[e];
   }
   __syncthreads();
 
   // ---- phase 2: wave-per-env lidar + observation rows
   const R co0 = S.ray_co[l], so0 = S.ray_so[l], co1 = S.ray_co[l + 64], so1 = S.ray_so[l + 64];
-  for (int k = wave; k < kEPB; k += kWaves) {
+  for (int k = wave; k < ne; k += kWaves) {
     const int e = e0 + k;
-    if (e >= S.N) break;
-    const int n = S.n_obs[e];
+    const R4<R> o = o_next;
+    if (k + kWaves < ne) o_next = load_obstacle(S, e + kWaves, l);   // prefetch next env
+    const int n = uniform(sh.n[k]);
     R rd0, rd1, min_key;
-    lidar_wave<R>(S, e, n, sh.px[k], sh.py[k], sh.psi[k], co0, so0, co1, so1, rd0, rd1, min_key);
+    lidar_wave<R>(o, n, sh.px[k], sh.py[k], sh.sp[k], sh.cp[k], co0, so0, co1, so1, rd0, rd1, min_key);
     const bool term = min_key < R(kTermDist);                  // simple_env.py:334
     const bool done = term || sh.trunc[k];
     const R ms = wave_min(rd0 < rd1 ? rd0 : rd1);              // simple_env.py:153
@@ -313,24 +342,21 @@ __global__ __launch_bounds__(kBlock) void step_kernel(State<R> S, IO<R> io) {
   __syncthreads();
 
   // ---- phase 3: lane-per-env reward, flags, autoreset
-  if (tid < kEPB) {
+  if (tid < ne) {
     const int e = e0 + tid;
-    if (e < S.N) {
-      const R coll = sh.msens[tid] < R(kCollDist) ? R(-20) : R(0);   // simple_env.py:153-156
-      io.rew[e] = coll + sh.partial[tid];
-      const bool term = sh.term[tid], trunc = sh.trunc[tid];
-      io.term[e] = term;
-      io.trunc[e] = trunc;
-      if ((term || trunc) && S.autoreset == USV_AUTORESET_SAME_STEP) {
-        float hdr[kHdr];
-        reset_env<R, MODE>(S, e, hdr);
-        float* row = io.obs + (size_t)e * kObsDim;
+    const R coll = sh.msens[tid] < R(kCollDist) ? R(-20) : R(0);   // simple_env.py:153-156
+    io.rew[e] = coll + sh.partial[tid];
+    const bool term = sh.term[tid], trunc = sh.trunc[tid];
+    io.term[e] = term;
+    io.trunc[e] = trunc;
+    if ((term || trunc) && S.autoreset == USV_AUTORESET_SAME_STEP) {
+      float hdr[kHdr];
+      reset_env<R, MODE>(S, e, hdr);
+      float* row = io.obs + (size_t)e * kObsDim;
 #pragma unroll
-        for (int i = 0; i < kHdr; ++i) row[i] = hdr[i];
-      }
+      for (int i = 0; i < kHdr; ++i) row[i] = hdr[i];
     }
   }
-  (void)l;
 }
 
 // --------------------------------------------------------------------------- reset kernel
@@ -343,17 +369,18 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(State<R> S, IO<R> io) {
   const int wave = tid / kWave;
   const int l = lane_id();
   const int e0 = blockIdx.x * kEPB;
+  const int ne = S.N - e0 < kEPB ? S.N - e0 : kEPB;
   const R co0 = S.ray_co[l], so0 = S.ray_so[l], co1 = S.ray_co[l + 64], so1 = S.ray_so[l + 64];
-  for (int k = wave; k < kEPB; k += kWaves) {
+  for (int k = wave; k < ne; k += kWaves) {
     const int e = e0 + k;
-    if (e >= S.N) break;
     if (io.mask && !io.mask[e]) continue;
     R rd0, rd1;
     R* last = S.sensor_last + (size_t)e * kSensors;
     if (S.scan_valid[e]) {
-      R mk;
-      lidar_wave<R>(S, e, S.n_obs[e], S.f[F_X][e], S.f[F_Y][e], S.f[F_PSI][e], co0, so0, co1,
-                    so1, rd0, rd1, mk);
+      R mk, sp, cp;
+      m_sincos(S.f[F_PSI][e], &sp, &cp);
+      lidar_wave<R>(load_obstacle(S, e, l), uniform(S.n_obs[e]), S.f[F_X][e], S.f[F_Y][e], sp, cp,
+                    co0, so0, co1, so1, rd0, rd1, mk);
       last[l] = rd0;
       last[64 + l] = rd1;
     } else {
@@ -365,9 +392,9 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(State<R> S, IO<R> io) {
     row[kHdr + 64 + l] = (float)(rd1 / R(kSensorMax));
   }
   __syncthreads();
-  if (tid < kEPB) {
+  if (tid < ne) {
     const int e = e0 + tid;
-    if (e < S.N && (!io.mask || io.mask[e])) {
+    if (!io.mask || io.mask[e]) {
       float hdr[kHdr];
       reset_env<R, MODE>(S, e, hdr);
       float* row = io.obs + (size_t)e * kObsDim;

@@ -61,12 +61,13 @@ def test_golden_trajectory_replay(golden, fname, env_id, precision):
     env = make(env_id, n, precision=precision, autoreset=False, max_episode_steps=max(limit, 0))
     env.set_state(golden_state(g))
     alive = np.ones(n, bool)
-    worst = {"obs": 0.0, "rew": 0.0}
+    worst = {"hdr": 0.0, "rew": 0.0}
+    flips, rays = 0, 0
     # f32 trajectories accumulate rounding along the rollout; ASMC adds 20 substeps per step
     if precision == "f64":
-        obs_tol, rew_tol = 2e-6, 1e-8
+        hdr_tol, sens_tol, rew_tol = 2e-6, 2e-6, 1e-8
     else:
-        obs_tol, rew_tol = (5e-4, 5e-3) if env_id == "usv-simple" else (2e-2, 5e-2)
+        hdr_tol, sens_tol, rew_tol = (5e-4, 1e-4, 5e-3) if env_id == "usv-simple" else (2e-2, 1e-3, 5e-2)
     for t in range(T):
         a = torch.from_numpy(g["actions"][:, t]).cuda()
         obs, rew, term, trunc, _ = env.step(a)
@@ -74,14 +75,19 @@ def test_golden_trajectory_replay(golden, fname, env_id, precision):
         m = alive
         if not m.any():
             break
-        d_obs = np.abs(obs[m] - g["final_obs"][m, t]).max()
-        d_rew = np.abs(rew[m] - g["reward"][m, t]).max()
-        worst["obs"], worst["rew"] = max(worst["obs"], d_obs), max(worst["rew"], d_rew)
+        ref = g["final_obs"][m, t]
+        worst["hdr"] = max(worst["hdr"], float(np.abs(obs[m, :15] - ref[:, :15]).max()))
+        worst["rew"] = max(worst["rew"], float(np.abs(rew[m] - g["reward"][m, t]).max()))
+        # a ray grazing an obstacle edge can flip hit/miss under fp32 rounding: count, bound
+        flips += int((np.abs(obs[m, 15:] - ref[:, 15:]) > sens_tol).sum())
+        rays += int(m.sum()) * 128
         np.testing.assert_array_equal(term[m], g["terminated"][m, t], err_msg=f"t={t}")
         np.testing.assert_array_equal(trunc[m], g["truncated"][m, t], err_msg=f"t={t}")
         alive = alive & ~(g["terminated"][:, t] | g["truncated"][:, t])
-    print(f"\n[golden {fname} {precision}] max |obs| err {worst['obs']:.3e}, max |rew| err {worst['rew']:.3e}")
-    assert worst["obs"] <= obs_tol and worst["rew"] <= rew_tol, worst
+    print(f"\n[golden {fname} {precision}] max |hdr| err {worst['hdr']:.3e}, max |rew| err "
+          f"{worst['rew']:.3e}, sensor flips {flips}/{rays}")
+    assert worst["hdr"] <= hdr_tol and worst["rew"] <= rew_tol, worst
+    assert flips <= (0 if precision == "f64" else max(2, rays // 10000))
     env.close()
 
 
@@ -200,30 +206,32 @@ def test_autoreset_semantics_and_time_limit():
     n, T, limit = 1024, 60, 25
     env = make("usv-simple", n, seed=7, max_episode_steps=limit)
     env.reset(seed=7)
-    torch.manual_seed(0)
+    gen = torch.Generator(device="cuda").manual_seed(0)
+    lo = torch.tensor([0.2, -1.0], device="cuda")
+    span = torch.tensor([0.8, 2.0], device="cuda")
+    age = np.zeros(n, np.int64)        # steps since this env's episode started
     ends = 0
-    last_u_prev = env.get_field("last_u")
     for t in range(T):
-        a = torch.rand(n, 2, device="cuda") * torch.tensor([0.8, 2.0], device="cuda") + torch.tensor([0.2, -1.0], device="cuda")
+        a = torch.rand(n, 2, device="cuda", generator=gen) * span + lo
         obs, rew, term, trunc, info = env.step(a)
         obs, term, trunc, fobs = to_np(obs, term, trunc, info["final_obs"])
+        age += 1
         done = term | trunc
+        # TimeLimit (gym_usv/__init__.py:27): truncated exactly when elapsed reaches the limit
+        assert np.all(trunc[age == limit]), t
         el = env.get_field("elapsed")
-        assert np.all(el[done] == 0) and np.all(el[~done] == ((t + 1) % limit if t + 1 >= limit else t + 1)) or True
+        np.testing.assert_array_equal(el[done], 0)
+        np.testing.assert_array_equal(el[~done], age[~done])
         if done.any():
             ends += int(done.sum())
             # reset obs keeps the terminal scan (stale sensor_data, simple_env.py:47,302)
             np.testing.assert_array_equal(obs[done, 15:], fobs[done, 15:])
             assert np.all(obs[done, 7:9] == 0)                 # _get_obs(zeros(3))
             assert np.all(obs[done, 5] == 0)                   # ye at path start
-            # last_action is NOT reset (reference quirk)
-            lu = env.get_field("last_u")
-            assert np.all(lu[done] != 0)
-        if t + 1 == limit:
-            assert np.all(done), "TimeLimit must end every episode at elapsed == limit"
-        last_u_prev = env.get_field("last_u")
-    assert ends > 0
-    del last_u_prev
+            # last_action is NOT reset (reference quirk): the next obs shows it again
+            assert np.all(env.get_field("last_u")[done] != 0)
+        age[done] = 0
+    assert ends > n                                             # every env hit the limit at least once
     env.close()
 
 
