@@ -108,6 +108,18 @@ __device__ __forceinline__ double bcast(double v, int lane) {
 }
 __device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
+template <typename R> struct Bits;
+template <> struct Bits<float> { using T = unsigned int; };
+template <> struct Bits<double> { using T = unsigned long long; };
+// ds_permute (push): this lane's value goes to lane `dst`; lanes nobody writes read 0.
+__device__ __forceinline__ unsigned int permute(int dst, unsigned int v) {
+  return (unsigned int)__builtin_amdgcn_ds_permute(dst << 2, (int)v);
+}
+__device__ __forceinline__ unsigned long long permute(int dst, unsigned long long v) {
+  const unsigned int lo = permute(dst, (unsigned int)v), hi = permute(dst, (unsigned int)(v >> 32));
+  return ((unsigned long long)hi << 32) | lo;
+}
+
 // DPP lane moves (gfx9 dpp_ctrl encodings): quad_perm [1,0,3,2], [2,3,0,1],
 // row_half_mirror, row_mirror.  Inactive/out-of-row sources keep `v` (bound_ctrl off).
 template <int CTRL> __device__ __forceinline__ float dpp(float v) {

@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -58,7 +59,8 @@ template <typename R> struct IO {
 
 constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / kWave;
-constexpr int kEPB = 64;   // envs per block
+constexpr int kEPBReset = 64;   // envs per block of the reset kernel
+constexpr int kLidDefault = 3;  // lidar variant of the reset kernel (all variants give identical scans)
 
 template <typename R> __device__ __forceinline__ R big() { return R(1e30); }
 
@@ -227,12 +229,27 @@ __device__ __forceinline__ void ray_pair(Ray<R>& ra, R jdx, R jdy, R jr2, R jk, 
   ra.bj = hit ? j : ra.bj;
 }
 
-template <typename R, bool RANGE_CHECK>
+// Lidar variants (compile-time): bit 0 = drop obstacles that lie wholly inside the rear
+// blind sector before the ray loop, bit 1 = obstacle loop unrolled by two.
+constexpr int kLidSkip = 1, kLidUnroll2 = 2;
+
+template <typename R, bool RANGE_CHECK, bool UNROLL2>
 __device__ __forceinline__ void ray_loop(Ray<R>& r0, Ray<R>& r1, R dx, R dy, R r2, R key, int n) {
-  for (int j = 0; j < n; ++j) {                  // n wave-uniform: scalar loop, v_readlane bcast
-    const R jdx = bcast(dx, j), jdy = bcast(dy, j), jr2 = bcast(r2, j), jk = bcast(key, j);
-    ray_pair<R, RANGE_CHECK>(r0, jdx, jdy, jr2, jk, j);
-    ray_pair<R, RANGE_CHECK>(r1, jdx, jdy, jr2, jk, j);
+  if (UNROLL2) {
+    for (int j = 0; j < n; j += 2) {             // n even (padded with a never-hit obstacle)
+      const R adx = bcast(dx, j), ady = bcast(dy, j), ar2 = bcast(r2, j), ak = bcast(key, j);
+      const R bdx = bcast(dx, j + 1), bdy = bcast(dy, j + 1), br2 = bcast(r2, j + 1), bk = bcast(key, j + 1);
+      ray_pair<R, RANGE_CHECK>(r0, adx, ady, ar2, ak, j);
+      ray_pair<R, RANGE_CHECK>(r1, adx, ady, ar2, ak, j);
+      ray_pair<R, RANGE_CHECK>(r0, bdx, bdy, br2, bk, j + 1);
+      ray_pair<R, RANGE_CHECK>(r1, bdx, bdy, br2, bk, j + 1);
+    }
+  } else {
+    for (int j = 0; j < n; ++j) {                // n wave-uniform: scalar loop, v_readlane bcast
+      const R jdx = bcast(dx, j), jdy = bcast(dy, j), jr2 = bcast(r2, j), jk = bcast(key, j);
+      ray_pair<R, RANGE_CHECK>(r0, jdx, jdy, jr2, jk, j);
+      ray_pair<R, RANGE_CHECK>(r1, jdx, jdy, jr2, jk, j);
+    }
   }
 }
 
@@ -246,23 +263,54 @@ __device__ __forceinline__ R ray_reading(const Ray<R>& ra, R dx, R dy, R r2) {
   return ra.bj >= 0 ? proj - m_sqrt(delta) : R(kSensorMax);                     // :457-459
 }
 
-template <typename R>
+// Rays span [psi - 120deg, psi + 118.125deg]; the blind sector between them has half-width
+// 60.9375deg around psi + 179.0625deg.  An obstacle (distance d > r) can be hit by no ray if
+// its angular extent [phi - a, phi + a], a = asin(r/d), lies inside that sector with a
+// 2-ray (3.75deg) margin:  dot(c - p, w) > cos(h)*sqrt(d^2 - r^2) + sin(h)*r  and r < d*sin(h)
+// with h = 57.1875deg.  Skipping such obstacles never changes a reading.
+constexpr double kBlindC = -0.99985057700379, kBlindS = 0.01636173162648;  // cos/sin(179.0625deg)
+constexpr double kBlindCosH = 0.54212310917132, kBlindSinH = 0.84029769328406;  // h = 57.1875deg
+
+template <typename R, int LID>
 __device__ __forceinline__ void lidar_wave(const R4<R>& o, int n, R px, R py, R sp, R cp, R co0,
                                            R so0, R co1, R so1, R& rd0, R& rd1, R& min_key) {
   const int l = lane_id();
   const bool valid = l < n;
-  const R dx = o.x - px, dy = o.y - py, r2 = o.w;
+  R dx = o.x - px, dy = o.y - py, r2 = o.w;
   const R d = m_sqrt(m_fma(dx, dx, dy * dy));
-  const R key = valid ? d - o.z : big<R>();                 // simple_env.py:205-206
+  R key = valid ? d - o.z : big<R>();                       // simple_env.py:205-206
   min_key = wave_min(key);
+  const R far = wave_max(valid ? d : R(0));
+  int m = n;
+  if (LID & kLidSkip) {
+    const R wx = cp * R(kBlindC) - sp * R(kBlindS), wy = sp * R(kBlindC) + cp * R(kBlindS);
+    const R rr = o.z;
+    const R dot = dx * wx + dy * wy;
+    const R lim = R(kBlindCosH) * m_sqrt(m_abs(d * d - rr * rr)) + R(kBlindSinH) * rr;
+    const bool blind = (d > rr) & (rr < d * R(kBlindSinH)) & (dot > lim);
+    const bool keep = valid & !blind;
+    // stream-compact the kept obstacles (order preserved, so min-key ties still resolve to
+    // the lowest original index)
+    const unsigned long long ball = __ballot(keep);
+    m = __popcll(ball);
+    const int pos = __builtin_amdgcn_mbcnt_hi((unsigned)(ball >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)ball, 0));
+    const int dst = keep ? pos : 63;               // dropped lanes all land in lane 63 (unused)
+    dx = __builtin_bit_cast(R, permute(dst, __builtin_bit_cast(typename Bits<R>::T, dx)));
+    dy = __builtin_bit_cast(R, permute(dst, __builtin_bit_cast(typename Bits<R>::T, dy)));
+    r2 = __builtin_bit_cast(R, permute(dst, __builtin_bit_cast(typename Bits<R>::T, r2)));
+    key = __builtin_bit_cast(R, permute(dst, __builtin_bit_cast(typename Bits<R>::T, key)));
+  }
+  if (LID & kLidUnroll2) {
+    if (l >= m) { r2 = R(-1); key = big<R>(); }    // padding obstacle: delta < 0, never hit
+    m = (m + 1) & ~1;
+  }
   // ray angle psi + (start + i*res) (usv_asmc_ca_env.py:420-423) by rotating the offset table
   Ray<R> r0{m_fma(cp, co0, -(sp * so0)), m_fma(sp, co0, cp * so0), big<R>(), -1};
   Ray<R> r1{m_fma(cp, co1, -(sp * so1)), m_fma(sp, co1, cp * so1), big<R>(), -1};
   // A reading is <= proj <= |c_j - p|; the reference's "< max range" test (:458) can only
   // reject when some obstacle is ~100 m away, so it is evaluated only then (wave-uniform).
-  const R far = wave_max(valid ? d : R(0));
-  if (far < R(0.99 * kSensorMax)) ray_loop<R, false>(r0, r1, dx, dy, r2, key, n);
-  else ray_loop<R, true>(r0, r1, dx, dy, r2, key, n);
+  if (far < R(0.99 * kSensorMax)) ray_loop<R, false, (LID & kLidUnroll2) != 0>(r0, r1, dx, dy, r2, key, m);
+  else ray_loop<R, true, (LID & kLidUnroll2) != 0>(r0, r1, dx, dy, r2, key, m);
   rd0 = ray_reading(r0, dx, dy, r2);
   rd1 = ray_reading(r1, dx, dy, r2);
 }
@@ -272,22 +320,22 @@ __device__ __forceinline__ R4<R> load_obstacle(const State<R>& S, int e, int l) 
   return l < S.cap ? S.obst[(size_t)e * S.cap + l] : R4<R>{R(0), R(0), R(0), R(0)};
 }
 
-template <typename R> struct Scratch {
-  float hdr[kHdr][kEPB + 1];
-  R px[kEPB], py[kEPB], sp[kEPB], cp[kEPB], partial[kEPB], msens[kEPB];
-  int n[kEPB];
-  uint8_t trunc[kEPB], term[kEPB];
+template <typename R, int EPB> struct Scratch {
+  float hdr[kHdr][EPB + 1];
+  R px[EPB], py[EPB], sp[EPB], cp[EPB], partial[EPB], msens[EPB];
+  int n[EPB];
+  uint8_t trunc[EPB], term[EPB];
 };
 
 // --------------------------------------------------------------------------- step kernel
-template <typename R, int MODE>
+template <typename R, int MODE, int EPB, int LID>
 __global__ __launch_bounds__(kBlock) void step_kernel(State<R> S, IO<R> io) {
-  __shared__ Scratch<R> sh;
+  __shared__ Scratch<R, EPB> sh;
   const int tid = threadIdx.x;
   const int wave = tid / kWave;
   const int l = lane_id();
-  const int e0 = blockIdx.x * kEPB;
-  const int ne = S.N - e0 < kEPB ? S.N - e0 : kEPB;   // envs of this block
+  const int e0 = blockIdx.x * EPB;
+  const int ne = S.N - e0 < EPB ? S.N - e0 : EPB;   // envs of this block
 
   // obstacle rows of this wave's first env: issued before phase 1 to overlap its latency
   R4<R> o_next = wave < ne ? load_obstacle(S, e0 + wave, l) : R4<R>{};
@@ -317,7 +365,7 @@ __global__ __launch_bounds__(kBlock) void step_kernel(State<R> S, IO<R> io) {
     if (k + kWaves < ne) o_next = load_obstacle(S, e + kWaves, l);   // prefetch next env
     const int n = uniform(sh.n[k]);
     R rd0, rd1, min_key;
-    lidar_wave<R>(o, n, sh.px[k], sh.py[k], sh.sp[k], sh.cp[k], co0, so0, co1, so1, rd0, rd1, min_key);
+    lidar_wave<R, LID>(o, n, sh.px[k], sh.py[k], sh.sp[k], sh.cp[k], co0, so0, co1, so1, rd0, rd1, min_key);
     const bool term = min_key < R(kTermDist);                  // simple_env.py:334
     const bool done = term || sh.trunc[k];
     const R ms = wave_min(rd0 < rd1 ? rd0 : rd1);              // simple_env.py:153
@@ -368,8 +416,8 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(State<R> S, IO<R> io) {
   const int tid = threadIdx.x;
   const int wave = tid / kWave;
   const int l = lane_id();
-  const int e0 = blockIdx.x * kEPB;
-  const int ne = S.N - e0 < kEPB ? S.N - e0 : kEPB;
+  const int e0 = blockIdx.x * kEPBReset;
+  const int ne = S.N - e0 < kEPBReset ? S.N - e0 : kEPBReset;
   const R co0 = S.ray_co[l], so0 = S.ray_so[l], co1 = S.ray_co[l + 64], so1 = S.ray_so[l + 64];
   for (int k = wave; k < ne; k += kWaves) {
     const int e = e0 + k;
@@ -379,7 +427,7 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(State<R> S, IO<R> io) {
     if (S.scan_valid[e]) {
       R mk, sp, cp;
       m_sincos(S.f[F_PSI][e], &sp, &cp);
-      lidar_wave<R>(load_obstacle(S, e, l), uniform(S.n_obs[e]), S.f[F_X][e], S.f[F_Y][e], sp, cp,
+      lidar_wave<R, kLidDefault>(load_obstacle(S, e, l), uniform(S.n_obs[e]), S.f[F_X][e], S.f[F_Y][e], sp, cp,
                     co0, so0, co1, so1, rd0, rd1, mk);
       last[l] = rd0;
       last[64 + l] = rd1;
@@ -435,6 +483,7 @@ const FieldDesc kFields[USV_FIELD_COUNT] = {
 struct Handle {
   usv_config cfg;
   int device;
+  int epb = 32, lid = 3;     // step-kernel variant (tuned default; see launch_step)
   void* slab = nullptr;
   State<float> sf{};
   State<double> sd{};
@@ -498,23 +547,45 @@ int carve(Handle* h, State<R>& S) {
   return USV_OK;
 }
 
+// Step-kernel variants: envs per block x lidar variant.  Selected per handle at create time
+// (USV_STEP_VARIANT="epb,lid" overrides, for tuning sweeps); all variants are bit-identical.
+using StepFnF = void (*)(State<float>, IO<float>);
+using StepFnD = void (*)(State<double>, IO<double>);
+constexpr int kEPBs[3] = {16, 32, 64};
+
+template <typename R, int MODE, int EPB>
+void* pick_lid(int lid) {
+  switch (lid) {
+    case 0: return (void*)&step_kernel<R, MODE, EPB, 0>;
+    case 1: return (void*)&step_kernel<R, MODE, EPB, 1>;
+    case 2: return (void*)&step_kernel<R, MODE, EPB, 2>;
+    default: return (void*)&step_kernel<R, MODE, EPB, 3>;
+  }
+}
+template <typename R, int MODE>
+void* pick_step(int epb, int lid) {
+  if (epb == 16) return pick_lid<R, MODE, 16>(lid);
+  if (epb == 32) return pick_lid<R, MODE, 32>(lid);
+  return pick_lid<R, MODE, 64>(lid);
+}
+
 template <typename R>
 int launch_step(Handle* h, State<R>& S, const float* act, float* obs, void* rew, uint8_t* term,
                 uint8_t* trunc, float* fobs, hipStream_t st) {
   IO<R> io{act, obs, (R*)rew, term, trunc, fobs, nullptr};
-  const dim3 grid((S.N + kEPB - 1) / kEPB), block(kBlock);
-  if (h->cfg.mode == USV_MODE_SIMPLE)
-    hipLaunchKernelGGL((step_kernel<R, USV_MODE_SIMPLE>), grid, block, 0, st, S, io);
-  else
-    hipLaunchKernelGGL((step_kernel<R, USV_MODE_ASMC_SIMPLE>), grid, block, 0, st, S, io);
-  HIP_TRY(hipGetLastError());
+  const int epb = h->epb, lid = h->lid;
+  void* fn = h->cfg.mode == USV_MODE_SIMPLE ? pick_step<R, USV_MODE_SIMPLE>(epb, lid)
+                                            : pick_step<R, USV_MODE_ASMC_SIMPLE>(epb, lid);
+  const dim3 grid((S.N + epb - 1) / epb), block(kBlock);
+  void* args[] = {(void*)&S, (void*)&io};
+  HIP_TRY(hipLaunchKernel(fn, grid, block, args, 0, st));
   return USV_OK;
 }
 
 template <typename R>
 int launch_reset(Handle* h, State<R>& S, const uint8_t* mask, float* obs, hipStream_t st) {
   IO<R> io{nullptr, obs, nullptr, nullptr, nullptr, nullptr, mask};
-  const dim3 grid((S.N + kEPB - 1) / kEPB), block(kBlock);
+  const dim3 grid((S.N + kEPBReset - 1) / kEPBReset), block(kBlock);
   if (h->cfg.mode == USV_MODE_SIMPLE)
     hipLaunchKernelGGL((reset_kernel<R, USV_MODE_SIMPLE>), grid, block, 0, st, S, io);
   else
@@ -658,6 +729,14 @@ int usv_create(const usv_config* cfg, int32_t device, void** out) {
   Handle* h = new Handle();
   h->cfg = *cfg;
   h->device = device;
+  if (const char* v = std::getenv("USV_STEP_VARIANT")) {   // "epb,lid" tuning override
+    int epb = 0, lid = 0;
+    if (std::sscanf(v, "%d,%d", &epb, &lid) == 2 && (epb == 16 || epb == 32 || epb == 64) &&
+        lid >= 0 && lid <= 3) {
+      h->epb = epb;
+      h->lid = lid;
+    }
+  }
   const int rc = cfg->precision == USV_F32 ? carve<float>(h, h->sf) : carve<double>(h, h->sd);
   if (rc != USV_OK) {
     if (h->slab) (void)hipFree(h->slab);
