@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <type_traits>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -25,7 +26,12 @@
 
 namespace usv {
 
-template <typename R> struct alignas(4 * sizeof(R)) R4 { R x, y, z, w; };
+// (x, y, r, r*r) of one obstacle as a native 4-vector (one 16-B / 32-B access, selectable in
+// registers without a stack temporary)
+template <typename R> struct V4;
+template <> struct V4<float> { typedef float T __attribute__((ext_vector_type(4))); };
+template <> struct V4<double> { typedef double T __attribute__((ext_vector_type(4))); };
+template <typename R> using R4 = typename V4<R>::T;
 
 enum RealField {
   F_X, F_Y, F_PSI, F_U, F_V, F_R, F_LAST_U, F_LAST_R, F_PROGRESS,
@@ -60,9 +66,12 @@ template <typename R> struct IO {
 constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / kWave;
 constexpr int kEPBReset = 64;   // envs per block of the reset kernel
-constexpr int kLidDefault = 3;  // lidar variant of the reset kernel (all variants give identical scans)
+constexpr int kLidDefault = 7;  // lidar variant of the reset kernel (all variants give identical scans)
 
 template <typename R> __device__ __forceinline__ R big() { return R(1e30); }
+template <typename R> struct Vec2;
+template <> struct Vec2<float> { using T = float2; };
+template <> struct Vec2<double> { using T = double2; };
 
 // obs[0:15] = [velocity/10, target_state(4), last_action[[0,2]]/max_action[[0,2]],
 //              max_action/10, max_acceleration/10]   (simple_env.py:72-96)
@@ -210,13 +219,22 @@ __device__ void env_dynamics(const State<R>& S, int e, float a_u, float a_r, flo
 
 // --------------------------------------------------------------------------- lidar
 // 128-ray lidar of one env at pose (px, py, heading sin/cos), wave-per-env.  Lane l owns rays
-// l and l+64; lane j holds obstacle j (`o`, already loaded).  Restates
-// compute_sensor_measurments / compute_obstacle_positions / _compute_sensor_distances
-// (usv_asmc_ca_env.py:411-461, 500-519): per ray, the hit obstacle with the smallest key
-// d_j = |c_j - p| - r_j, which equals the reference's first hit in argsort(d) order.
-// Every product is an explicit fma or a rounded multiply, so the step and reset kernels
-// produce bit-identical scans (the stale-scan reset obs depends on it).
+// l and l+64; lane j holds obstacle j (`o`).  Restates compute_sensor_measurments /
+// compute_obstacle_positions / _compute_sensor_distances (usv_asmc_ca_env.py:411-461,
+// 500-519): per ray, the hit obstacle with the smallest key d_j = |c_j - p| - r_j, which is
+// the reference's first hit in argsort(d) order.  Every product is an explicit fma or a
+// rounded multiply and every variant evaluates the identical per-(ray, obstacle) arithmetic,
+// so all variants -- and the step and reset kernels -- produce bit-identical scans.
 template <typename R> struct Ray { R c, s, bk; int bj; };
+
+template <typename R> __device__ __forceinline__ R l_sqrt(R x) { return m_sqrt(x); }
+template <> __device__ __forceinline__ float l_sqrt(float x) { return __builtin_amdgcn_sqrtf(x); }
+template <typename R> __device__ __forceinline__ R l_norm(R x) { return x / R(kSensorMax); }
+template <> __device__ __forceinline__ float l_norm(float x) { return x * 0.01f; }
+
+// ray direction = rotation of the ray-offset table entry (start + i*res) by the heading
+template <typename R> __device__ __forceinline__ R ray_c(R cp, R sp, R co, R so) { return m_fma(cp, co, -(sp * so)); }
+template <typename R> __device__ __forceinline__ R ray_s(R cp, R sp, R co, R so) { return m_fma(sp, co, cp * so); }
 
 template <typename R, bool RANGE_CHECK>
 __device__ __forceinline__ void ray_pair(Ray<R>& ra, R jdx, R jdy, R jr2, R jk, int j) {
@@ -224,14 +242,15 @@ __device__ __forceinline__ void ray_pair(Ray<R>& ra, R jdx, R jdy, R jr2, R jk, 
   const R perp = m_fma(jdx, ra.s, -(jdy * ra.c)); // obstacle y, mirrored (:518)
   const R delta = m_fma(-perp, perp, jr2);        // r^2 - y^2 (:453)
   bool hit = (proj >= R(0)) & (delta >= R(0)) & (jk < ra.bk);
-  if (RANGE_CHECK) hit = hit && (proj - m_sqrt(delta)) < R(kSensorMax);   // :458
+  if (RANGE_CHECK) hit = hit && (proj - l_sqrt(delta)) < R(kSensorMax);   // :458
   ra.bk = hit ? jk : ra.bk;
   ra.bj = hit ? j : ra.bj;
 }
 
-// Lidar variants (compile-time): bit 0 = drop obstacles that lie wholly inside the rear
-// blind sector before the ray loop, bit 1 = obstacle loop unrolled by two.
-constexpr int kLidSkip = 1, kLidUnroll2 = 2;
+// Lidar variants (compile-time): bit 0 = drop obstacles wholly inside the rear blind sector
+// before the ray loop, bit 1 = obstacle loop unrolled by two, bit 2 = angular-window pair
+// expansion (f32; falls back to bits 0|1 for f64 and when an obstacle is ~100 m away).
+constexpr int kLidSkip = 1, kLidUnroll2 = 2, kLidWindow = 4;
 
 template <typename R, bool RANGE_CHECK, bool UNROLL2>
 __device__ __forceinline__ void ray_loop(Ray<R>& r0, Ray<R>& r1, R dx, R dy, R r2, R key, int n) {
@@ -254,13 +273,13 @@ __device__ __forceinline__ void ray_loop(Ray<R>& r0, Ray<R>& r1, R dx, R dy, R r
 }
 
 template <typename R>
-__device__ __forceinline__ R ray_reading(const Ray<R>& ra, R dx, R dy, R r2) {
-  const int src = ra.bj < 0 ? 0 : ra.bj;
+__device__ __forceinline__ R reading_of(R c, R s, int bj, R dx, R dy, R r2) {
+  const int src = bj < 0 ? 0 : bj;
   const R gdx = __shfl(dx, src, kWave), gdy = __shfl(dy, src, kWave), gr2 = __shfl(r2, src, kWave);
-  const R proj = m_fma(gdx, ra.c, gdy * ra.s);
-  const R perp = m_fma(gdx, ra.s, -(gdy * ra.c));
+  const R proj = m_fma(gdx, c, gdy * s);
+  const R perp = m_fma(gdx, s, -(gdy * c));
   const R delta = m_fma(-perp, perp, gr2);
-  return ra.bj >= 0 ? proj - m_sqrt(delta) : R(kSensorMax);                     // :457-459
+  return bj >= 0 ? proj - l_sqrt(delta) : R(kSensorMax);                        // :457-459
 }
 
 // Rays span [psi - 120deg, psi + 118.125deg]; the blind sector between them has half-width
@@ -270,23 +289,54 @@ __device__ __forceinline__ R ray_reading(const Ray<R>& ra, R dx, R dy, R r2) {
 // with h = 57.1875deg.  Skipping such obstacles never changes a reading.
 constexpr double kBlindC = -0.99985057700379, kBlindS = 0.01636173162648;  // cos/sin(179.0625deg)
 constexpr double kBlindCosH = 0.54212310917132, kBlindSinH = 0.84029769328406;  // h = 57.1875deg
+constexpr double kRes = (4.0 * kPi / 3.0) / kSensors;
+constexpr double kStartC = -0.5, kStartS = -0.86602540378443865;                 // cos/sin(-120deg)
+
+// Per-env lidar outputs: readings of this lane's two rays and the three wave-uniform flags the
+// step needs (simple_env.py:153-155, :334; the "< max range" test of :458 only matters if an
+// obstacle is ~100 m away).
+template <typename R> struct Scan { R rd0, rd1; bool term, far; };
+
+// |atan2(y, x)| error < 2e-5 rad (minimax on [0,1] + octant folding); only used to size the
+// conservative ray windows, never for a reading.
+__device__ __forceinline__ float fast_atan2(float y, float x) {
+  const float ax = fabsf(x), ay = fabsf(y);
+  const float mx = fmaxf(fmaxf(ax, ay), 1e-30f), mn = fminf(ax, ay);
+  const float t = mn * __builtin_amdgcn_rcpf(mx);
+  const float s = t * t;
+  float p = fmaf(fmaf(fmaf(fmaf(0.0208351f, s, -0.085133f), s, 0.180141f), s, -0.3302995f), s, 0.999866f) * t;
+  p = ay > ax ? 1.57079633f - p : p;
+  p = x < 0.0f ? 3.14159265f - p : p;
+  return y < 0.0f ? -p : p;
+}
+
+__device__ __forceinline__ unsigned ord_key(float k) {   // float -> order-preserving uint
+  const unsigned u = __float_as_uint(k);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+// Inclusive prefix sum over the 64 lanes (DPP row scans + row carries).
+__device__ __forceinline__ int wave_incl_scan(int v) {
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, true);   // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, true);   // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, true);   // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, true);   // row_shr:8
+  const int l = lane_id();
+  const int t0 = __builtin_amdgcn_readlane(v, 15), t1 = __builtin_amdgcn_readlane(v, 31);
+  const int t2 = __builtin_amdgcn_readlane(v, 47);
+  return v + (l >= 16 ? t0 : 0) + (l >= 32 ? t1 : 0) + (l >= 48 ? t2 : 0);
+}
 
 template <typename R, int LID>
-__device__ __forceinline__ void lidar_wave(const R4<R>& o, int n, R px, R py, R sp, R cp, R co0,
-                                           R so0, R co1, R so1, R& rd0, R& rd1, R& min_key) {
+__device__ __forceinline__ void lidar_brute(R dx, R dy, R r2, R key, R d, R rr, bool valid, int n,
+                                            bool far, R sp, R cp, R co0, R so0, R co1, R so1,
+                                            Scan<R>& out) {
   const int l = lane_id();
-  const bool valid = l < n;
-  R dx = o.x - px, dy = o.y - py, r2 = o.w;
-  const R d = m_sqrt(m_fma(dx, dx, dy * dy));
-  R key = valid ? d - o.z : big<R>();                       // simple_env.py:205-206
-  min_key = wave_min(key);
-  const R far = wave_max(valid ? d : R(0));
   int m = n;
   if (LID & kLidSkip) {
     const R wx = cp * R(kBlindC) - sp * R(kBlindS), wy = sp * R(kBlindC) + cp * R(kBlindS);
-    const R rr = o.z;
     const R dot = dx * wx + dy * wy;
-    const R lim = R(kBlindCosH) * m_sqrt(m_abs(d * d - rr * rr)) + R(kBlindSinH) * rr;
+    const R lim = R(kBlindCosH) * l_sqrt(m_abs(d * d - rr * rr)) + R(kBlindSinH) * rr;
     const bool blind = (d > rr) & (rr < d * R(kBlindSinH)) & (dot > lim);
     const bool keep = valid & !blind;
     // stream-compact the kept obstacles (order preserved, so min-key ties still resolve to
@@ -304,73 +354,190 @@ __device__ __forceinline__ void lidar_wave(const R4<R>& o, int n, R px, R py, R 
     if (l >= m) { r2 = R(-1); key = big<R>(); }    // padding obstacle: delta < 0, never hit
     m = (m + 1) & ~1;
   }
-  // ray angle psi + (start + i*res) (usv_asmc_ca_env.py:420-423) by rotating the offset table
-  Ray<R> r0{m_fma(cp, co0, -(sp * so0)), m_fma(sp, co0, cp * so0), big<R>(), -1};
-  Ray<R> r1{m_fma(cp, co1, -(sp * so1)), m_fma(sp, co1, cp * so1), big<R>(), -1};
-  // A reading is <= proj <= |c_j - p|; the reference's "< max range" test (:458) can only
-  // reject when some obstacle is ~100 m away, so it is evaluated only then (wave-uniform).
-  if (far < R(0.99 * kSensorMax)) ray_loop<R, false, (LID & kLidUnroll2) != 0>(r0, r1, dx, dy, r2, key, m);
+  Ray<R> r0{ray_c(cp, sp, co0, so0), ray_s(cp, sp, co0, so0), big<R>(), -1};
+  Ray<R> r1{ray_c(cp, sp, co1, so1), ray_s(cp, sp, co1, so1), big<R>(), -1};
+  if (!far) ray_loop<R, false, (LID & kLidUnroll2) != 0>(r0, r1, dx, dy, r2, key, m);
   else ray_loop<R, true, (LID & kLidUnroll2) != 0>(r0, r1, dx, dy, r2, key, m);
-  rd0 = ray_reading(r0, dx, dy, r2);
-  rd1 = ray_reading(r1, dx, dy, r2);
+  out.rd0 = reading_of(r0.c, r0.s, r0.bj, dx, dy, r2);
+  out.rd1 = reading_of(r1.c, r1.s, r1.bj, dx, dy, r2);
 }
 
-template <typename R>
-__device__ __forceinline__ R4<R> load_obstacle(const State<R>& S, int e, int l) {
-  return l < S.cap ? S.obst[(size_t)e * S.cap + l] : R4<R>{R(0), R(0), R(0), R(0)};
+// Angular-window lidar (f32).  Lane j computes the ray-index windows its obstacle can touch
+// (conservative: +1.5 rays of margin around asin(r/d), pi/2 when the boat is inside it), the
+// (obstacle, ray) pairs are expanded over the lanes (prefix sum + per-lane binary search), each
+// pair runs the same exact test as the brute loop, and the hit with the smallest
+// (key, index) per ray wins through an LDS ds_min_u64 -- the min-key rule, bit-identical to
+// lidar_brute.  ~100 pair tests per env instead of 128 x n.
+__device__ __forceinline__ void lidar_window(float dx, float dy, float r2, float key, float d, float rr,
+                                             bool valid, int n, float sp, float cp, const float2* rayoff,
+                                             unsigned long long* slot, Scan<float>& out) {
+  const int l = lane_id();
+  const float c0r = ray_c(cp, sp, (float)kStartC, (float)kStartS);
+  const float s0r = ray_s(cp, sp, (float)kStartC, (float)kStartS);
+  const float a = dx * c0r + dy * s0r, b = dy * c0r - dx * s0r;
+  const float phi = fast_atan2(b, a);                 // CCW angle from ray 0; ray i at i*res
+  const float margin = (float)(1.5 * kRes);
+  const bool inside = d <= rr * 1.001f;
+  const float half = inside ? (float)(kPi / 2) + margin
+                            : fast_atan2(rr, __builtin_amdgcn_sqrtf(fmaxf(d * d - rr * rr, 0.0f))) + margin;
+  const float inv = (float)(1.0 / kRes);
+  const int lo1 = max(0, (int)ceilf((phi - half) * inv)), hi1 = min(127, (int)floorf((phi + half) * inv));
+  const float phi2 = phi + (float)(2 * kPi);
+  const int lo2 = max(0, (int)ceilf((phi2 - half) * inv)), hi2 = min(127, (int)floorf((phi2 + half) * inv));
+  const int len1 = valid ? max(0, hi1 - lo1 + 1) : 0, len2 = valid ? max(0, hi2 - lo2 + 1) : 0;
+  const int cnt = len1 + len2;
+  const int incl = wave_incl_scan(cnt);
+  const int off = incl - cnt;
+  const int W = __builtin_amdgcn_readlane(incl, 63);
+  const int off_s = valid ? off : (1 << 24);          // lanes without an obstacle are never owners
+  const int meta = lo1 | (len1 << 8) | (lo2 << 16);
+  const unsigned ok = ord_key(key);
+  for (int base = 0; base < W; base += kWave) {       // wave-uniform pass count
+    const int q = base + l;
+    int j = 0;
+#pragma unroll
+    for (int step = 32; step >= 1; step >>= 1) {      // largest j with off_j <= q
+      const int cand = j + step;
+      const int ov = __shfl(off_s, cand & 63, kWave);
+      j = (cand < kWave && ov <= q) ? cand : j;
+    }
+    const int k = q - __shfl(off, j, kWave);
+    const int mj = __shfl(meta, j, kWave);
+    const int l1 = mj & 255, n1 = (mj >> 8) & 255, l2 = mj >> 16;
+    int i = k < n1 ? l1 + k : l2 + (k - n1);
+    i = min(max(i, 0), 127);
+    const float gdx = __shfl(dx, j, kWave), gdy = __shfl(dy, j, kWave), gr2 = __shfl(r2, j, kWave);
+    const unsigned gk = (unsigned)__shfl((int)ok, j, kWave);
+    const float2 cs = rayoff[i];
+    const float c = ray_c(cp, sp, cs.x, cs.y), s = ray_s(cp, sp, cs.x, cs.y);
+    const float proj = fmaf(gdx, c, gdy * s);
+    const float perp = fmaf(gdx, s, -(gdy * c));
+    const float delta = fmaf(-perp, perp, gr2);
+    if ((q < W) & (proj >= 0.0f) & (delta >= 0.0f))
+      atomicMin(&slot[i], ((unsigned long long)gk << 32) | (unsigned)j);
+  }
+  const unsigned long long v0 = slot[l], v1 = slot[l + 64];
+  slot[l] = ~0ull;                                    // re-arm for this wave's next env
+  slot[l + 64] = ~0ull;
+  const float2 cs0 = rayoff[l], cs1 = rayoff[l + 64];
+  const int j0 = v0 == ~0ull ? -1 : (int)(unsigned)v0, j1 = v1 == ~0ull ? -1 : (int)(unsigned)v1;
+  out.rd0 = reading_of(ray_c(cp, sp, cs0.x, cs0.y), ray_s(cp, sp, cs0.x, cs0.y), j0, dx, dy, r2);
+  out.rd1 = reading_of(ray_c(cp, sp, cs1.x, cs1.y), ray_s(cp, sp, cs1.x, cs1.y), j1, dx, dy, r2);
+  (void)n;
 }
 
-template <typename R, int EPB> struct Scratch {
+template <typename R, int LID>
+__device__ __forceinline__ void lidar_wave(const R4<R>& o, int n, R px, R py, R sp, R cp,
+                                           const typename Vec2<R>::T* rayoff, unsigned long long* slot,
+                                           Scan<R>& out) {
+  const int l = lane_id();
+  const bool valid = l < n;
+  const R dx = o.x - px, dy = o.y - py, r2 = o.w, rr = o.z;
+  const R d = l_sqrt(m_fma(dx, dx, dy * dy));
+  const R key = valid ? d - rr : big<R>();                                      // simple_env.py:205-206
+  out.term = __ballot(valid & (key < R(kTermDist))) != 0;                       // :334
+  out.far = __ballot(valid & (d >= R(0.99 * kSensorMax))) != 0;
+  if constexpr (std::is_same<R, float>::value && (LID & kLidWindow) != 0) {
+    if (!out.far) {
+      lidar_window(dx, dy, r2, key, d, rr, valid, n, sp, cp, rayoff, slot, out);
+      return;
+    }
+  }
+  const auto t0 = rayoff[l], t1 = rayoff[l + 64];
+  lidar_brute<R, LID & (kLidSkip | kLidUnroll2)>(dx, dy, r2, key, d, rr, valid, n, out.far, sp, cp,
+                                                  t0.x, t0.y, t1.x, t1.y, out);
+}
+
+template <typename R, int EPB> struct alignas(16) Scratch {
   float hdr[kHdr][EPB + 1];
-  R px[EPB], py[EPB], sp[EPB], cp[EPB], partial[EPB], msens[EPB];
+  R px[EPB], py[EPB], sp[EPB], cp[EPB], partial[EPB];
   int n[EPB];
-  uint8_t trunc[EPB], term[EPB];
+  uint8_t trunc[EPB], term[EPB], coll[EPB];
 };
+
+// Dynamic LDS carve: [ray offset table 128 x Vec2][per-wave pair slots 4 x 128 x u64]
+//                    [obstacle rows EPB x cap x R4]
+template <typename R> __host__ __device__ constexpr size_t lds_rayoff_bytes() { return 128 * 2 * sizeof(R); }
+constexpr size_t kLdsSlotBytes = (size_t)kWaves * 128 * 8;
+template <typename R> __host__ __device__ size_t lds_bytes(int epb, int cap) {
+  return lds_rayoff_bytes<R>() + kLdsSlotBytes + (size_t)epb * cap * sizeof(R4<R>);
+}
+
+// Block prologue shared by the step and reset kernels: ray-offset table and slot init.
+template <typename R>
+__device__ __forceinline__ void lds_prologue(const State<R>& S, char* lds, int tid) {
+  auto* rayoff = reinterpret_cast<typename Vec2<R>::T*>(lds);
+  auto* slots = reinterpret_cast<unsigned long long*>(lds + lds_rayoff_bytes<R>());
+  if (tid < kSensors) rayoff[tid] = typename Vec2<R>::T{S.ray_co[tid], S.ray_so[tid]};
+  for (int i = tid; i < kWaves * 128; i += kBlock) slots[i] = ~0ull;
+}
 
 // --------------------------------------------------------------------------- step kernel
 template <typename R, int MODE, int EPB, int LID>
 __global__ __launch_bounds__(kBlock) void step_kernel(State<R> S, IO<R> io) {
   __shared__ Scratch<R, EPB> sh;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  auto* rayoff = reinterpret_cast<typename Vec2<R>::T*>(lds);
+  auto* slots = reinterpret_cast<unsigned long long*>(lds + lds_rayoff_bytes<R>());
+  R4<R>* lobst = reinterpret_cast<R4<R>*>(lds + lds_rayoff_bytes<R>() + kLdsSlotBytes);
   const int tid = threadIdx.x;
   const int wave = tid / kWave;
   const int l = lane_id();
   const int e0 = blockIdx.x * EPB;
   const int ne = S.N - e0 < EPB ? S.N - e0 : EPB;   // envs of this block
+  const int cap = S.cap;
 
-  // obstacle rows of this wave's first env: issued before phase 1 to overlap its latency
-  R4<R> o_next = wave < ne ? load_obstacle(S, e0 + wave, l) : R4<R>{};
-
-  // ---- phase 1: lane-per-env dynamics
-  if (tid < ne) {
-    const int e = e0 + tid;
-    const float2 a = reinterpret_cast<const float2*>(io.act)[e];
-    float hdr[kHdr];
-    R px, py, sp, cp, partial;
-    bool trunc;
-    env_dynamics<R, MODE>(S, e, a.x, a.y, hdr, px, py, sp, cp, partial, trunc);
+  lds_prologue(S, lds, tid);
+  if (tid < kWave) {
+    // ---- phase 1 (wave 0): lane-per-env dynamics
+    if (tid < ne) {
+      const int e = e0 + tid;
+      const float2 a = reinterpret_cast<const float2*>(io.act)[e];
+      float hdr[kHdr];
+      R px, py, sp, cp, partial;
+      bool trunc;
+      env_dynamics<R, MODE>(S, e, a.x, a.y, hdr, px, py, sp, cp, partial, trunc);
 #pragma unroll
-    for (int i = 0; i < kHdr; ++i) sh.hdr[i][tid] = hdr[i];
-    sh.px[tid] = px; sh.py[tid] = py; sh.sp[tid] = sp; sh.cp[tid] = cp;
-    sh.partial[tid] = partial;
-    sh.trunc[tid] = trunc;
-    sh.n[tid] = S.n_obs[e];
+      for (int i = 0; i < kHdr; ++i) sh.hdr[i][tid] = hdr[i];
+      sh.px[tid] = px; sh.py[tid] = py; sh.sp[tid] = sp; sh.cp[tid] = cp;
+      sh.partial[tid] = partial;
+      sh.trunc[tid] = trunc;
+      sh.n[tid] = S.n_obs[e];
+    }
+  } else {
+    // ---- phase 1 (waves 1..3): stage this block's obstacle rows in LDS meanwhile
+    // rows k = wave-1, wave+2, ...; four loads in flight before their LDS stores
+    const R4<R>* src = S.obst + (size_t)e0 * cap + l;
+    const R4<R> z{R(0), R(0), R(0), R(0)};
+    const bool lane_ok = l < cap;
+    for (int k = wave - 1; k < ne; k += 4 * (kWaves - 1)) {
+      const int k1 = k + (kWaves - 1), k2 = k + 2 * (kWaves - 1), k3 = k + 3 * (kWaves - 1);
+      const R4<R> b0 = lane_ok ? src[(size_t)k * cap] : z;
+      const R4<R> b1 = lane_ok && k1 < ne ? src[(size_t)k1 * cap] : z;
+      const R4<R> b2 = lane_ok && k2 < ne ? src[(size_t)k2 * cap] : z;
+      const R4<R> b3 = lane_ok && k3 < ne ? src[(size_t)k3 * cap] : z;
+      if (lane_ok) {
+        lobst[k * cap + l] = b0;
+        if (k1 < ne) lobst[k1 * cap + l] = b1;
+        if (k2 < ne) lobst[k2 * cap + l] = b2;
+        if (k3 < ne) lobst[k3 * cap + l] = b3;
+      }
+    }
   }
   __syncthreads();
 
   // ---- phase 2: wave-per-env lidar + observation rows
-  const R co0 = S.ray_co[l], so0 = S.ray_so[l], co1 = S.ray_co[l + 64], so1 = S.ray_so[l + 64];
+  unsigned long long* wslot = slots + wave * 128;
   for (int k = wave; k < ne; k += kWaves) {
     const int e = e0 + k;
-    const R4<R> o = o_next;
-    if (k + kWaves < ne) o_next = load_obstacle(S, e + kWaves, l);   // prefetch next env
     const int n = uniform(sh.n[k]);
-    R rd0, rd1, min_key;
-    lidar_wave<R, LID>(o, n, sh.px[k], sh.py[k], sh.sp[k], sh.cp[k], co0, so0, co1, so1, rd0, rd1, min_key);
-    const bool term = min_key < R(kTermDist);                  // simple_env.py:334
-    const bool done = term || sh.trunc[k];
-    const R ms = wave_min(rd0 < rd1 ? rd0 : rd1);              // simple_env.py:153
-    if (l == 0) { sh.term[k] = term; sh.msens[k] = ms; }
-    const float s0 = (float)(rd0 / R(kSensorMax)), s1 = (float)(rd1 / R(kSensorMax));  // :82-83
+    const R4<R> o = l < n ? lobst[k * cap + l] : R4<R>{R(0), R(0), R(0), R(0)};
+    Scan<R> sc;
+    lidar_wave<R, LID>(o, n, sh.px[k], sh.py[k], sh.sp[k], sh.cp[k], rayoff, wslot, sc);
+    const bool done = sc.term || sh.trunc[k];
+    const bool coll = __ballot((sc.rd0 < R(kCollDist)) | (sc.rd1 < R(kCollDist))) != 0;  // :153-156
+    if (l == 0) { sh.term[k] = sc.term; sh.coll[k] = coll; }
+    const float s0 = (float)l_norm(sc.rd0), s1 = (float)l_norm(sc.rd1);          // :82-83
     const bool reset_now = done && S.autoreset == USV_AUTORESET_SAME_STEP;
     float* row = io.obs + (size_t)e * kObsDim;
     row[kHdr + l] = s0;                                        // stale scan is kept by reset
@@ -383,8 +550,8 @@ __global__ __launch_bounds__(kBlock) void step_kernel(State<R> S, IO<R> io) {
       if (l < kHdr) f[l] = sh.hdr[l][k];
     }
     if (reset_now) {
-      S.sensor_last[(size_t)e * kSensors + l] = rd0;
-      S.sensor_last[(size_t)e * kSensors + 64 + l] = rd1;
+      S.sensor_last[(size_t)e * kSensors + l] = sc.rd0;
+      S.sensor_last[(size_t)e * kSensors + 64 + l] = sc.rd1;
     }
   }
   __syncthreads();
@@ -392,7 +559,7 @@ __global__ __launch_bounds__(kBlock) void step_kernel(State<R> S, IO<R> io) {
   // ---- phase 3: lane-per-env reward, flags, autoreset
   if (tid < ne) {
     const int e = e0 + tid;
-    const R coll = sh.msens[tid] < R(kCollDist) ? R(-20) : R(0);   // simple_env.py:153-156
+    const R coll = sh.coll[tid] ? R(-20) : R(0);                    // simple_env.py:153-156
     io.rew[e] = coll + sh.partial[tid];
     const bool term = sh.term[tid], trunc = sh.trunc[tid];
     io.term[e] = term;
@@ -413,22 +580,30 @@ __global__ __launch_bounds__(kBlock) void step_kernel(State<R> S, IO<R> io) {
 // current one, else the stored one; zeros for a never-stepped env), simple_env.py:302.
 template <typename R, int MODE>
 __global__ __launch_bounds__(kBlock) void reset_kernel(State<R> S, IO<R> io) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  auto* rayoff = reinterpret_cast<typename Vec2<R>::T*>(lds);
+  auto* slots = reinterpret_cast<unsigned long long*>(lds + lds_rayoff_bytes<R>());
   const int tid = threadIdx.x;
   const int wave = tid / kWave;
   const int l = lane_id();
   const int e0 = blockIdx.x * kEPBReset;
   const int ne = S.N - e0 < kEPBReset ? S.N - e0 : kEPBReset;
-  const R co0 = S.ray_co[l], so0 = S.ray_so[l], co1 = S.ray_co[l + 64], so1 = S.ray_so[l + 64];
+  lds_prologue(S, lds, tid);
+  __syncthreads();
   for (int k = wave; k < ne; k += kWaves) {
     const int e = e0 + k;
     if (io.mask && !io.mask[e]) continue;
     R rd0, rd1;
     R* last = S.sensor_last + (size_t)e * kSensors;
     if (S.scan_valid[e]) {
-      R mk, sp, cp;
+      R sp, cp;
       m_sincos(S.f[F_PSI][e], &sp, &cp);
-      lidar_wave<R, kLidDefault>(load_obstacle(S, e, l), uniform(S.n_obs[e]), S.f[F_X][e], S.f[F_Y][e], sp, cp,
-                    co0, so0, co1, so1, rd0, rd1, mk);
+      const int n = uniform(S.n_obs[e]);
+      const R4<R> o = l < n ? S.obst[(size_t)e * S.cap + l] : R4<R>{R(0), R(0), R(0), R(0)};
+      Scan<R> sc;
+      lidar_wave<R, kLidDefault>(o, n, S.f[F_X][e], S.f[F_Y][e], sp, cp, rayoff, slots + wave * 128, sc);
+      rd0 = sc.rd0;
+      rd1 = sc.rd1;
       last[l] = rd0;
       last[64 + l] = rd1;
     } else {
@@ -436,8 +611,8 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(State<R> S, IO<R> io) {
       rd1 = last[64 + l];
     }
     float* row = io.obs + (size_t)e * kObsDim;
-    row[kHdr + l] = (float)(rd0 / R(kSensorMax));
-    row[kHdr + 64 + l] = (float)(rd1 / R(kSensorMax));
+    row[kHdr + l] = (float)l_norm(rd0);
+    row[kHdr + 64 + l] = (float)l_norm(rd1);
   }
   __syncthreads();
   if (tid < ne) {
@@ -559,7 +734,9 @@ void* pick_lid(int lid) {
     case 0: return (void*)&step_kernel<R, MODE, EPB, 0>;
     case 1: return (void*)&step_kernel<R, MODE, EPB, 1>;
     case 2: return (void*)&step_kernel<R, MODE, EPB, 2>;
-    default: return (void*)&step_kernel<R, MODE, EPB, 3>;
+    case 3: return (void*)&step_kernel<R, MODE, EPB, 3>;
+    case 5: return (void*)&step_kernel<R, MODE, EPB, 5>;
+    default: return (void*)&step_kernel<R, MODE, EPB, 7>;
   }
 }
 template <typename R, int MODE>
@@ -578,7 +755,7 @@ int launch_step(Handle* h, State<R>& S, const float* act, float* obs, void* rew,
                                             : pick_step<R, USV_MODE_ASMC_SIMPLE>(epb, lid);
   const dim3 grid((S.N + epb - 1) / epb), block(kBlock);
   void* args[] = {(void*)&S, (void*)&io};
-  HIP_TRY(hipLaunchKernel(fn, grid, block, args, 0, st));
+  HIP_TRY(hipLaunchKernel(fn, grid, block, args, lds_bytes<R>(epb, S.cap), st));
   return USV_OK;
 }
 
@@ -587,9 +764,9 @@ int launch_reset(Handle* h, State<R>& S, const uint8_t* mask, float* obs, hipStr
   IO<R> io{nullptr, obs, nullptr, nullptr, nullptr, nullptr, mask};
   const dim3 grid((S.N + kEPBReset - 1) / kEPBReset), block(kBlock);
   if (h->cfg.mode == USV_MODE_SIMPLE)
-    hipLaunchKernelGGL((reset_kernel<R, USV_MODE_SIMPLE>), grid, block, 0, st, S, io);
+    hipLaunchKernelGGL((reset_kernel<R, USV_MODE_SIMPLE>), grid, block, lds_bytes<R>(0, S.cap), st, S, io);
   else
-    hipLaunchKernelGGL((reset_kernel<R, USV_MODE_ASMC_SIMPLE>), grid, block, 0, st, S, io);
+    hipLaunchKernelGGL((reset_kernel<R, USV_MODE_ASMC_SIMPLE>), grid, block, lds_bytes<R>(0, S.cap), st, S, io);
   HIP_TRY(hipGetLastError());
   return USV_OK;
 }
@@ -636,12 +813,11 @@ int field_io(Handle* h, State<R>& S, int f, void* host, bool to_host) {
     HIP_TRY(hipMemcpy(tmp.data(), S.obst, cnt * sizeof(R4<R>), hipMemcpyDeviceToHost));
     double* hd = (double*)host;
     for (size_t i = 0; i < cnt; ++i) {
-      R4<R>& o = tmp[i];
-      R& c = f == USV_FIELD_OBS_X ? o.x : f == USV_FIELD_OBS_Y ? o.y : o.z;
-      if (to_host) hd[i] = (double)c;
+      const int ci = f - USV_FIELD_OBS_X;      // component x / y / r
+      if (to_host) hd[i] = (double)tmp[i][ci];
       else {
-        c = (R)hd[i];
-        if (f == USV_FIELD_OBS_R) o.w = o.z * o.z;
+        tmp[i][ci] = (R)hd[i];
+        if (f == USV_FIELD_OBS_R) tmp[i][3] = tmp[i][2] * tmp[i][2];
       }
     }
     if (!to_host) HIP_TRY(hipMemcpy(S.obst, tmp.data(), cnt * sizeof(R4<R>), hipMemcpyHostToDevice));
@@ -732,7 +908,7 @@ int usv_create(const usv_config* cfg, int32_t device, void** out) {
   if (const char* v = std::getenv("USV_STEP_VARIANT")) {   // "epb,lid" tuning override
     int epb = 0, lid = 0;
     if (std::sscanf(v, "%d,%d", &epb, &lid) == 2 && (epb == 16 || epb == 32 || epb == 64) &&
-        lid >= 0 && lid <= 3) {
+        lid >= 0 && lid <= 7) {
       h->epb = epb;
       h->lid = lid;
     }

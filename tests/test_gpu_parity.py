@@ -310,3 +310,30 @@ def test_single_env_api():
     obs, r, term, trunc, info = env.step(np.array([0.5, 0.0], dtype=np.float32))
     assert isinstance(r, float) and isinstance(term, bool) and isinstance(trunc, bool)
     env.close()
+
+
+@pytest.mark.parametrize("env_id,precision", [("usv-simple", "f32"), ("usv-simple", "f64"),
+                                              ("usv-asmc-simple", "f32")])
+def test_step_variants_bit_identical(env_id, precision, monkeypatch):
+    """Every step-kernel variant (envs/block, blind-sector skip, unroll, angular-window pair
+    expansion) must give bit-identical outputs: pruning only removes pairs that cannot hit."""
+    n, T = 2048, 24
+    gen = torch.Generator(device="cuda").manual_seed(9)
+    acts = [torch.rand(n, 2, device="cuda", generator=gen) * torch.tensor([0.8, 2.0], device="cuda")
+            + torch.tensor([0.2, -1.0], device="cuda") for _ in range(T)]
+    ref = None
+    for v in ("64,0", "16,1", "32,3", "32,5", "32,7", "64,7"):
+        monkeypatch.setenv("USV_STEP_VARIANT", v)
+        env = make(env_id, n, seed=4, precision=precision)
+        env.reset(seed=4)
+        outs = []
+        for a in acts:
+            o, r, te, tr, info = env.step(a)
+            outs.append((o.clone(), r.clone(), te.clone(), tr.clone()))
+        env.close()
+        if ref is None:
+            ref = outs
+            continue
+        for t, (a_, b_) in enumerate(zip(ref, outs)):
+            for x, y in zip(a_, b_):
+                assert torch.equal(x, y), f"variant {v} differs at step {t}"

@@ -52,7 +52,7 @@ def main():
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--env-id", default="usv-simple")
     ap.add_argument("--precision", default="f32")
-    ap.add_argument("--variants", default="16,0 16,3 32,0 32,1 32,2 32,3 64,0 64,1 64,2 64,3")
+    ap.add_argument("--variants", default="64,0 32,1 32,3 16,5 32,5 64,5 16,7 32,7 64,7")
     args = ap.parse_args()
     g = torch.Generator(device="cuda").manual_seed(0)
     acts = [torch.rand(args.envs, 2, device="cuda", generator=g) * torch.tensor([0.8, 2.0], device="cuda")
