@@ -658,7 +658,7 @@ const FieldDesc kFields[USV_FIELD_COUNT] = {
 struct Handle {
   usv_config cfg;
   int device;
-  int epb = 32, lid = 3;     // step-kernel variant (tuned default; see launch_step)
+  int epb = 32, lid = 7;     // step-kernel variant (tuned default; see launch_step)
   void* slab = nullptr;
   State<float> sf{};
   State<double> sd{};
@@ -878,7 +878,7 @@ void usv_config_default(usv_config* cfg, int32_t mode, int32_t num_envs) {
   cfg->obstacle_cap = 32;
   cfg->max_episode_steps = mode == USV_MODE_ASMC_SIMPLE ? 1000 : 500;   // gym_usv/__init__.py:27,33
   cfg->autoreset = USV_AUTORESET_SAME_STEP;
-  cfg->lidar_algo = USV_LIDAR_BRUTE;
+  cfg->lidar_algo = USV_LIDAR_WINDOW;
   cfg->seed = 0;
   cfg->env_id_offset = 0;
 }
