@@ -93,6 +93,10 @@ template <typename T> __device__ __forceinline__ T wrap_angle(T a) {  // simple_
   m_sincos(a, &s, &c);
   return m_atan2(s, c);
 }
+// f32 build: atan2(sin a, cos a) == a - 2 pi rint(a / 2 pi) up to rounding (|err| ~ ulp(a))
+template <> __device__ __forceinline__ float wrap_angle(float a) {
+  return fmaf(-6.28318548f, rintf(a * 0.159154943f), a);
+}
 
 // ----------------------------------------------------------------------------- wave helpers
 __device__ __forceinline__ int lane_id() { return __lane_id(); }

@@ -75,73 +75,121 @@ template <> struct Vec2<double> { using T = double2; };
 
 // obs[0:15] = [velocity/10, target_state(4), last_action[[0,2]]/max_action[[0,2]],
 //              max_action/10, max_acceleration/10]   (simple_env.py:72-96)
+// x / c for a compile-time constant c: exact division in the f64 build, a multiply by the
+// rounded reciprocal (<= 1 ulp) in the f32 build.
+template <typename R> __device__ __forceinline__ R cdiv(R x, double c) { return x / R(c); }
+template <> __device__ __forceinline__ float cdiv(float x, double c) { return x * (float)(1.0 / c); }
+
 template <typename R>
 __device__ __forceinline__ void make_header(float (&h)[kHdr], R u, R v, R r, R angle, R dist,
                                             R ye, R refv, R act_u, R act_r, R mu, R mr) {
-  h[0] = (float)(u / R(10)); h[1] = (float)(v / R(10)); h[2] = (float)(r / R(10));
-  h[3] = (float)(angle / R(kPi)); h[4] = (float)(dist / R(kDiag));
-  h[5] = (float)(ye / R(10)); h[6] = (float)(refv / R(10));
+  h[0] = (float)cdiv(u, 10); h[1] = (float)cdiv(v, 10); h[2] = (float)cdiv(r, 10);
+  h[3] = (float)cdiv(angle, kPi); h[4] = (float)cdiv(dist, kDiag);
+  h[5] = (float)cdiv(ye, 10); h[6] = (float)cdiv(refv, 10);
   h[7] = (float)(act_u / mu); h[8] = (float)(act_r / mr);
-  h[9] = (float)(mu / R(10)); h[10] = 0.0f; h[11] = (float)(mr / R(10));
+  h[9] = (float)cdiv(mu, 10); h[10] = 0.0f; h[11] = (float)cdiv(mr, 10);
   h[12] = (float)(kMaxAccU / 10.0); h[13] = 0.0f; h[14] = (float)(kMaxAccR / 10.0);
 }
 
 // --------------------------------------------------------------------------- reset
-// In-kernel episode reset of env e (lane-per-env), distributionally identical to
-// UsvSimpleEnv.reset (simple_env.py:228-308); writes the reset-obs header.
-// last_action is NOT reset (reference quirk), sensor_data stays stale.
-template <typename R, int MODE>
-__device__ void reset_env(const State<R>& S, int e, float (&hdr)[kHdr]) {
-  const int ep = S.episode[e];
-  Philox g(S.seed, S.gid0 + (uint64_t)e, (uint32_t)ep);
-  const double sx = g.normal(kBound / 2, 0.5), sy = g.normal(kBound / 2, 0.5);   // :234-235
-  const double psi = g.uniform(-kPi, kPi);                                        // :238
-  const double ang = g.uniform(-kPi, kPi), dist = g.uniform(100.0, 110.0);        // :241-242
-  const double ex = sx + cos(ang) * dist, ey = sy + sin(ang) * dist;              // :243
-  const double tx = g.uniform(0.0, kBound), ty = g.uniform(0.0, kBound);          // :245
-  const double u = g.uniform(0.0, 0.15), v = g.uniform(0.0, 0.15), r = g.uniform(0.0, 0.15);  // :246
-  const double mu = g.uniform(1.5, 3.0);                                          // :249
-  const double mr = g.uniform(3.0, 6.0);                                          // :250
-  const double refv = g.uniform(0.75, mu);                                        // :251
-  const int n = g.integers(15, 30);                                               // :257
-  R4<R>* ob = S.obst + (size_t)e * S.cap;
-  int k = 0;
-  for (int j = 0; j < n; ++j) {                                                   // :258-268
-    const double ox = g.uniform(0.0, kBound), oy = g.uniform(0.0, kBound);
-    if (hypot(sx - ox, sy - oy) < 0.5 || hypot(tx - ox, ty - oy) < 0.5) continue;
-    const double rad = g.uniform(0.15, 0.5);                                      // :290
-    ob[k++] = R4<R>{R(ox), R(oy), R(rad), R(rad) * R(rad)};
-  }
-  if (k == 0) {                                                                   // :270-274
-    const double ox = g.uniform(0.0, kBound), oy = g.uniform(0.0, kBound);
-    const double rad = g.uniform(0.15, 0.5);
-    ob[k++] = R4<R>{R(ox), R(oy), R(rad), R(rad) * R(rad)};
-  }
-  for (int j = k; j < S.cap; ++j) ob[j] = R4<R>{R(0), R(0), R(0), R(0)};
-  const R x = R(sx), y = R(sy), p = R(psi);
-  S.f[F_X][e] = x; S.f[F_Y][e] = y; S.f[F_PSI][e] = p;
-  S.f[F_U][e] = R(u); S.f[F_V][e] = R(v); S.f[F_R][e] = R(r);
-  S.f[F_PROGRESS][e] = R(0);
-  S.f[F_PX0][e] = x; S.f[F_PY0][e] = y; S.f[F_PX1][e] = R(ex); S.f[F_PY1][e] = R(ey);
-  S.f[F_MAX_U][e] = R(mu); S.f[F_MAX_R][e] = R(mr); S.f[F_REF_V][e] = R(refv);
-  S.n_obs[e] = k;
-  S.elapsed[e] = 0;
-  S.episode[e] = ep + 1;
-  S.scan_valid[e] = 0;
-  if (MODE == USV_MODE_ASMC_SIMPLE) {                                             // simple_env_asmc.py:15
+// In-kernel episode reset of env e, executed by one whole wave (wave-parallel), and
+// distributionally identical to UsvSimpleEnv.reset (simple_env.py:228-308).
+//
+// Random numbers: lane l runs two Philox4x32-10 blocks keyed by the run seed with counter
+// (global env id, episode, l) and (global env id, episode, l + 64): four 53-bit uniforms
+// U[l][0..3].  Lane j < 32 draws obstacle j (x, y, radius); lanes 32..36 draw the scalars.
+// The reference's draw order cannot be reproduced with Philox anyway (PCG64 + ziggurat), so
+// parity of resets is distributional (KS tests); the stream is fixed per (seed, env, episode),
+// independent of sharding, precision and kernel.
+// last_action is NOT reset (reference quirk) and sensor_data stays stale (the caller keeps the
+// scan in the obs row).  Writes the reset-obs header into row[0:15].
+// Four uniforms in [0, 1) per lane: one Philox block (24-bit floats) for the f32 build, two
+// blocks (53-bit doubles) for the f64 build.
+template <typename R> struct Uni4 { R u[4]; };
+__device__ __forceinline__ void philox_uniforms(Philox& g, int l, Uni4<float>& o) {
+  uint32_t a[4];
+  g.c3 = (uint32_t)l;
+  g.block(a[0], a[1], a[2], a[3]);
 #pragma unroll
-    for (int i = 0; i < kAsmcN; ++i) S.asmc[(size_t)i * S.N + e] = R(0);
+  for (int i = 0; i < 4; ++i) o.u[i] = (float)(a[i] >> 8) * (1.0f / 16777216.0f);
+}
+__device__ __forceinline__ void philox_uniforms(Philox& g, int l, Uni4<double>& o) {
+  uint32_t a[4], b[4];
+  g.c3 = (uint32_t)l;
+  g.block(a[0], a[1], a[2], a[3]);
+  g.c3 = (uint32_t)l + 64u;
+  g.block(b[0], b[1], b[2], b[3]);
+  const double k = 1.0 / 9007199254740992.0;
+  o.u[0] = (double)((((uint64_t)a[0] << 32) | a[1]) >> 11) * k;
+  o.u[1] = (double)((((uint64_t)a[2] << 32) | a[3]) >> 11) * k;
+  o.u[2] = (double)((((uint64_t)b[0] << 32) | b[1]) >> 11) * k;
+  o.u[3] = (double)((((uint64_t)b[2] << 32) | b[3]) >> 11) * k;
+}
+
+template <typename R, int MODE>
+__device__ __forceinline__ void reset_wave(const State<R>& S, int e, float* row) {
+  const int l = lane_id();
+  const int ep = uniform(S.episode[e]);
+  Philox g(S.seed, S.gid0 + (uint64_t)e, (uint32_t)ep);
+  Uni4<R> U;
+  philox_uniforms(g, l, U);
+  // scalar draws (uniform across the wave, held in SGPRs):
+  //   lane 32: path-start normal pair (Box-Muller) (:234-235), psi (:238), path angle (:241)
+  //   lane 33: path length (:242), target x, y (:245), u0 (:246)
+  //   lane 34: v0, r0 (:246), max_action[0] (:249), max_action[2] (:250)
+  //   lane 35: ref_v (:251), obstacle count (:257), fallback obstacle x, y (:273)
+  //   lane 36: fallback obstacle radius (:290)
+  const R bm = m_sqrt(R(-2) * log(R(1) - bcast(U.u[0], 32)));
+  R sb, cb;
+  m_sincos(R(2 * kPi) * bcast(U.u[1], 32), &sb, &cb);
+  const R sx = R(kBound / 2) + R(0.5) * bm * cb, sy = R(kBound / 2) + R(0.5) * bm * sb;
+  const R tx = R(kBound) * bcast(U.u[1], 33), ty = R(kBound) * bcast(U.u[2], 33);
+  const R mu = R(1.5) + R(1.5) * bcast(U.u[2], 34);
+  const int n = min(15 + (int)(bcast(U.u[1], 35) * R(15)), 29);
+  // obstacles: lane j < n draws (x, y) in [0, 20]^2 (:258) and its radius (:290); drop those
+  // within 0.5 of the start or the target (:261-268), order kept; none left -> one fallback
+  const R ox = R(kBound) * U.u[0], oy = R(kBound) * U.u[1], orad = R(0.15) + R(0.35) * U.u[2];
+  const bool keep = (l < n) && !(m_hypot(sx - ox, sy - oy) < R(0.5) || m_hypot(tx - ox, ty - oy) < R(0.5));
+  const unsigned long long ball = __ballot(keep);
+  int cnt = __popcll(ball);
+  const int pos = __builtin_amdgcn_mbcnt_hi((unsigned)(ball >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)ball, 0));
+  R4<R>* ob = S.obst + (size_t)e * S.cap;
+  if (keep) ob[pos] = R4<R>{ox, oy, orad, orad * orad};
+  if (cnt == 0) {
+    const R fx = R(kBound) * bcast(U.u[2], 35), fy = R(kBound) * bcast(U.u[3], 35);
+    const R fr = R(0.15) + R(0.35) * bcast(U.u[0], 36);
+    if (l == 0) ob[0] = R4<R>{fx, fy, fr, fr * fr};
+    cnt = 1;
   }
-  // reset obs: _get_obs(zeros(3)) with the random target_position (:302, :72-80)
-  const R rtx = R(tx), rty = R(ty);
-  const R angle = wrap_angle(m_atan2(rty - y, rtx - x) - p);
-  const R dst = m_hypot(x - rtx, y - rty);
-  const R dx = R(ex) - x, dy = R(ey) - y;
-  const R ak = m_atan2(dy, dx);
-  R sak, cak;
-  m_sincos(ak, &sak, &cak);
-  const R ye = -(x - x) * sak + (y - y) * cak;                                    // :133-137
-  make_header<R>(hdr, R(u), R(v), R(r), angle, dst, ye, R(refv), R(0), R(0), R(mu), R(mr));
+  if (l >= cnt && l < S.cap) ob[l] = R4<R>{R(0), R(0), R(0), R(0)};
+  if (MODE == USV_MODE_ASMC_SIMPLE && l < kAsmcN) S.asmc[(size_t)l * S.N + e] = R(0);  // simple_env_asmc.py:15
+  if (l == 0) {
+    const R psi = R(-kPi) + R(2 * kPi) * bcast(U.u[2], 32), ang = R(-kPi) + R(2 * kPi) * bcast(U.u[3], 32);
+    const R dist = R(100) + R(10) * bcast(U.u[0], 33);
+    const R u = R(0.15) * bcast(U.u[3], 33), v = R(0.15) * bcast(U.u[0], 34), r = R(0.15) * bcast(U.u[1], 34);
+    const R mr = R(3) + R(3) * bcast(U.u[3], 34);
+    const R refv = R(0.75) + (mu - R(0.75)) * bcast(U.u[0], 35);
+    R sa, ca;
+    m_sincos(ang, &sa, &ca);
+    S.f[F_X][e] = sx; S.f[F_Y][e] = sy; S.f[F_PSI][e] = psi;
+    S.f[F_U][e] = u; S.f[F_V][e] = v; S.f[F_R][e] = r;
+    S.f[F_PROGRESS][e] = R(0);
+    S.f[F_PX0][e] = sx; S.f[F_PY0][e] = sy;
+    S.f[F_PX1][e] = sx + ca * dist; S.f[F_PY1][e] = sy + sa * dist;                // :243
+    S.f[F_MAX_U][e] = mu; S.f[F_MAX_R][e] = mr; S.f[F_REF_V][e] = refv;
+    S.n_obs[e] = cnt;
+    S.elapsed[e] = 0;
+    S.episode[e] = ep + 1;
+    S.scan_valid[e] = 0;
+    // reset obs: _get_obs(zeros(3)) with the random target_position (:302, :72-80); position
+    // == path_start, so ye == 0 exactly
+    const R angle = wrap_angle(m_atan2(ty - sy, tx - sx) - psi);
+    const R dst = m_hypot(sx - tx, sy - ty);
+    float h[kHdr];
+    make_header<R>(h, u, v, r, angle, dst, R(0), refv, R(0), R(0), mu, mr);
+#pragma unroll
+    for (int i = 0; i < kHdr; ++i) row[i] = h[i];
+  }
 }
 
 // --------------------------------------------------------------------------- phase 1
@@ -200,7 +248,7 @@ __device__ void env_dynamics(const State<R>& S, int e, float a_u, float a_r, flo
   make_header<R>(hdr, u, v, r, angle, dist, ye, refv, lu, lr, mu, mr);   // obs uses PREVIOUS action
   // _get_reward without the collision term (:150-186)
   const R dact = m_abs(lu - a3u) + m_abs(lr - a3r);
-  const R yk = ye / R(kYeK);
+  const R yk = cdiv(ye, kYeK);
   const R e1 = m_exp(-m_abs(yk)), e2 = m_exp(-(yk * yk));
   const R ye_r = e1 > e2 ? e1 : e2;
   const R ang_r = m_exp(-m_abs(angle));
@@ -496,7 +544,12 @@ __global__ __launch_bounds__(kBlock) void step_kernel(State<R> S, IO<R> io) {
       float hdr[kHdr];
       R px, py, sp, cp, partial;
       bool trunc;
+#ifdef USV_DIAG_NODYN
+      px = S.f[F_X][e] + a.x; py = S.f[F_Y][e] + a.y; sp = R(0.5); cp = R(0.8); partial = R(0); trunc = false;
+      for (int i = 0; i < kHdr; ++i) hdr[i] = (float)px;
+#else
       env_dynamics<R, MODE>(S, e, a.x, a.y, hdr, px, py, sp, cp, partial, trunc);
+#endif
 #pragma unroll
       for (int i = 0; i < kHdr; ++i) sh.hdr[i][tid] = hdr[i];
       sh.px[tid] = px; sh.py[tid] = py; sh.sp[tid] = sp; sh.cp[tid] = cp;
@@ -533,7 +586,11 @@ __global__ __launch_bounds__(kBlock) void step_kernel(State<R> S, IO<R> io) {
     const int n = uniform(sh.n[k]);
     const R4<R> o = l < n ? lobst[k * cap + l] : R4<R>{R(0), R(0), R(0), R(0)};
     Scan<R> sc;
+#ifdef USV_DIAG_NOLIDAR
+    sc.rd0 = sc.rd1 = R(kSensorMax) + o.x; sc.term = false; sc.far = false;
+#else
     lidar_wave<R, LID>(o, n, sh.px[k], sh.py[k], sh.sp[k], sh.cp[k], rayoff, wslot, sc);
+#endif
     const bool done = sc.term || sh.trunc[k];
     const bool coll = __ballot((sc.rd0 < R(kCollDist)) | (sc.rd1 < R(kCollDist))) != 0;  // :153-156
     if (l == 0) { sh.term[k] = sc.term; sh.coll[k] = coll; }
@@ -554,9 +611,14 @@ __global__ __launch_bounds__(kBlock) void step_kernel(State<R> S, IO<R> io) {
       S.sensor_last[(size_t)e * kSensors + 64 + l] = sc.rd1;
     }
   }
+  // same-step autoreset of this wave's done envs (own loop: keeps the lidar loop's registers free)
+  if (S.autoreset == USV_AUTORESET_SAME_STEP) {
+    for (int k = wave; k < ne; k += kWaves)
+      if (sh.term[k] | sh.trunc[k]) reset_wave<R, MODE>(S, e0 + k, io.obs + (size_t)(e0 + k) * kObsDim);
+  }
   __syncthreads();
 
-  // ---- phase 3: lane-per-env reward, flags, autoreset
+  // ---- phase 3: lane-per-env reward and flags (coalesced)
   if (tid < ne) {
     const int e = e0 + tid;
     const R coll = sh.coll[tid] ? R(-20) : R(0);                    // simple_env.py:153-156
@@ -564,13 +626,6 @@ __global__ __launch_bounds__(kBlock) void step_kernel(State<R> S, IO<R> io) {
     const bool term = sh.term[tid], trunc = sh.trunc[tid];
     io.term[e] = term;
     io.trunc[e] = trunc;
-    if ((term || trunc) && S.autoreset == USV_AUTORESET_SAME_STEP) {
-      float hdr[kHdr];
-      reset_env<R, MODE>(S, e, hdr);
-      float* row = io.obs + (size_t)e * kObsDim;
-#pragma unroll
-      for (int i = 0; i < kHdr; ++i) row[i] = hdr[i];
-    }
   }
 }
 
@@ -613,17 +668,7 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(State<R> S, IO<R> io) {
     float* row = io.obs + (size_t)e * kObsDim;
     row[kHdr + l] = (float)l_norm(rd0);
     row[kHdr + 64 + l] = (float)l_norm(rd1);
-  }
-  __syncthreads();
-  if (tid < ne) {
-    const int e = e0 + tid;
-    if (!io.mask || io.mask[e]) {
-      float hdr[kHdr];
-      reset_env<R, MODE>(S, e, hdr);
-      float* row = io.obs + (size_t)e * kObsDim;
-#pragma unroll
-      for (int i = 0; i < kHdr; ++i) row[i] = hdr[i];
-    }
+    reset_wave<R, MODE>(S, e, row);
   }
 }
 
@@ -724,9 +769,6 @@ int carve(Handle* h, State<R>& S) {
 
 // Step-kernel variants: envs per block x lidar variant.  Selected per handle at create time
 // (USV_STEP_VARIANT="epb,lid" overrides, for tuning sweeps); all variants are bit-identical.
-using StepFnF = void (*)(State<float>, IO<float>);
-using StepFnD = void (*)(State<double>, IO<double>);
-constexpr int kEPBs[3] = {16, 32, 64};
 
 template <typename R, int MODE, int EPB>
 void* pick_lid(int lid) {

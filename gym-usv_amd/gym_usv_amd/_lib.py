@@ -11,6 +11,8 @@ import os
 
 LIB_NAME = "libusvhip.so"
 LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
+# diagnostic builds (tools/) may point at another in-tree copy of the library
+LIB_PATH = os.environ.get("USV_LIB_PATH", LIB_PATH)
 
 ABI_VERSION = 1
 MODE_SIMPLE, MODE_ASMC_SIMPLE = 0, 1
