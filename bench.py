@@ -87,7 +87,7 @@ def main():
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
     ap.add_argument("--env-id", default="usv-simple", choices=["usv-simple", "usv-asmc-simple"])
     ap.add_argument("--precision", default="f32", choices=["f32", "f64"])
-    ap.add_argument("--lidar", default="brute", choices=["brute", "window"])
+    ap.add_argument("--lidar", default="window", choices=["brute", "window"])
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-procs", type=int, default=0, help="0 = min(16, available cores)")

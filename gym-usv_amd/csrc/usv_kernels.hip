@@ -947,6 +947,7 @@ int usv_create(const usv_config* cfg, int32_t device, void** out) {
   Handle* h = new Handle();
   h->cfg = *cfg;
   h->device = device;
+  h->lid = cfg->lidar_algo == USV_LIDAR_BRUTE ? (kLidSkip | kLidUnroll2) : (kLidSkip | kLidUnroll2 | kLidWindow);
   if (const char* v = std::getenv("USV_STEP_VARIANT")) {   // "epb,lid" tuning override
     int epb = 0, lid = 0;
     if (std::sscanf(v, "%d,%d", &epb, &lid) == 2 && (epb == 16 || epb == 32 || epb == 64) &&

@@ -46,7 +46,7 @@ class UsvVectorEnv:
     metadata = {"render_modes": [], "autoreset_mode": "same-step"}
 
     def __init__(self, env_id="usv-simple", num_envs=4096, device=0, seed=0, precision="f32",
-                 autoreset=True, max_episode_steps=None, obstacle_cap=32, lidar="brute",
+                 autoreset=True, max_episode_steps=None, obstacle_cap=32, lidar="window",
                  env_id_offset=0):
         if env_id not in ENV_SPECS:
             raise ValueError(f"unknown env id {env_id!r}; known: {sorted(ENV_SPECS)}")

@@ -1,0 +1,68 @@
+"""Summarise rocprofv3 outputs for the step kernel into profiles/<round>_summary.json and
+profiles/pmc_summary.json (read by bench.py for roofline.traffic).
+
+    python tools/pmc_summary.py --kt DIR --fetch DIR --write DIR --key usv-simple/65536/f32/window --round r01
+
+FETCH_SIZE / WRITE_SIZE are in KiB per dispatch (TCC_EA0_RDREQ/WRREQ based, include Infinity
+Cache hits).  On gfx950 FETCH_SIZE under-counts wide (16 B/lane) streaming reads by 2x
+(MI355X_MICROARCH.md, HBM section); this kernel's reads are mostly 4-B/lane SoA loads plus
+16-B obstacle rows, so both the raw value and the 2x-corrected upper bound are recorded and the
+raw (lower) one is used.
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+
+
+def rows(d, pattern):
+    f = glob.glob(os.path.join(d, "**", pattern), recursive=True)
+    if not f:
+        raise SystemExit(f"no {pattern} under {d}")
+    return list(csv.DictReader(open(f[0])))
+
+
+def counter(d, name, kernel="step_kernel", skip=5):
+    vals = [float(r["Counter_Value"]) for r in rows(d, "*counter_collection.csv")
+            if kernel in r["Kernel_Name"] and r["Counter_Name"] == name]
+    vals = vals[skip:] or vals
+    return sum(vals) / len(vals), len(vals)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--kt", required=True)
+    ap.add_argument("--fetch", required=True)
+    ap.add_argument("--write", required=True)
+    ap.add_argument("--key", required=True)
+    ap.add_argument("--round", default="r01")
+    ap.add_argument("--out", default="profiles")
+    a = ap.parse_args()
+    stats = [r for r in rows(a.kt, "*kernel_stats.csv")]
+    step = [r for r in stats if "step_kernel" in r["Name"]]
+    fetch_kib, nf = counter(a.fetch, "FETCH_SIZE")
+    write_kib, nw = counter(a.write, "WRITE_SIZE")
+    summ = {
+        "key": a.key,
+        "kernel_stats": [{k: r[k] for k in ("Name", "Calls", "AverageNs", "MinNs", "MaxNs", "Percentage")}
+                         for r in stats[:8]],
+        "step_kernel_avg_ns": float(step[0]["AverageNs"]) if step else None,
+        "fetch_kib_per_launch": fetch_kib, "write_kib_per_launch": write_kib,
+        "fetch_samples": nf, "write_samples": nw,
+        "hbm_bytes_per_launch": round((fetch_kib + write_kib) * 1024),
+        "hbm_bytes_per_launch_fetch_x2": round((2 * fetch_kib + write_kib) * 1024),
+    }
+    os.makedirs(a.out, exist_ok=True)
+    json.dump(summ, open(os.path.join(a.out, f"{a.round}_summary.json"), "w"), indent=1)
+    agg_p = os.path.join(a.out, "pmc_summary.json")
+    agg = json.load(open(agg_p)) if os.path.exists(agg_p) else {}
+    agg[a.key] = {"hbm_bytes_per_launch": summ["hbm_bytes_per_launch"],
+                  "hbm_bytes_per_launch_fetch_x2": summ["hbm_bytes_per_launch_fetch_x2"],
+                  "step_kernel_avg_ns": summ["step_kernel_avg_ns"], "round": a.round}
+    json.dump(agg, open(agg_p, "w"), indent=1)
+    print(json.dumps(summ, indent=1))
+
+
+if __name__ == "__main__":
+    main()
