@@ -48,6 +48,29 @@ def algorithmic_bytes_per_env_step(env_id, mean_obs, precision="f32"):
     return act + obs + rew + flags + state_rd + state_wr + obst + asmc
 
 
+# --------------------------------------------------------------------------- multi-rank plumbing
+def shard(rank, envs_per_rank):
+    """Global env ids owned by `rank`: [rank*N, (rank+1)*N) (DESIGN.md 'Multi-GPU').  The reset
+    RNG is keyed by global id, so results do not depend on the number of ranks."""
+    return rank * envs_per_rank, (rank + 1) * envs_per_rank
+
+
+def reduce_max(values, device=None):
+    """Max over ranks of a few floats (elapsed time, kernel time); identity when not distributed."""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return [float(v) for v in values]
+    t = torch.tensor(values, dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(v) for v in t.tolist()]
+
+
+def aggregate_rate(envs_per_rank, world, steps, max_elapsed):
+    """Whole-job env-steps/s: every rank's env-steps over the slowest rank's time (weak scaling)."""
+    return envs_per_rank * world * steps / max_elapsed
+
+
 # --------------------------------------------------------------------------- CPU baseline
 def _cpu_worker(args):
     env_id, seconds, seed = args
@@ -111,7 +134,7 @@ def main():
     import gym_usv_amd
     N, K, W = args.envs, args.steps, args.warmup
     env = gym_usv_amd.make_vec(args.env_id, N, device=local, seed=args.seed, precision=args.precision,
-                               lidar=args.lidar, env_id_offset=rank * N)
+                               lidar=args.lidar, env_id_offset=shard(rank, N)[0])
     env.reset(seed=args.seed)
     mean_obs = float(env.get_field("n_obs").mean())
 
@@ -157,14 +180,10 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     kern_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
-    if world > 1:
-        t = torch.tensor([elapsed, kern_ms], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0]), float(t[1])
+    elapsed, kern_ms = reduce_max([elapsed, kern_ms], device=dev)
 
     if rank == 0:
-        total_env_steps = N * world * K
-        value = total_env_steps / elapsed
+        value = aggregate_rate(N, world, K, elapsed)
         bpe = algorithmic_bytes_per_env_step(args.env_id, mean_obs, args.precision)
         bytes_per_launch = bpe * N
         achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9

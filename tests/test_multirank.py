@@ -1,0 +1,47 @@
+"""World-size-2 gloo test of the multi-GPU bench plumbing on CPU: env sharding by global id,
+max-over-ranks timing and the whole-job rate (bench.py)."""
+import os
+import socket
+
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    lo, hi = bench.shard(rank, 1000)
+    # each rank reports a different elapsed; every rank must see the max
+    el, km = bench.reduce_max([1.0 + rank, 0.5 * (rank + 1)])
+    rate = bench.aggregate_rate(1000, world, 10, el)
+    q.put((rank, lo, hi, el, km, rate))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_sharding_and_timing():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    assert [(r[1], r[2]) for r in res] == [(0, 1000), (1000, 2000)]     # disjoint, contiguous shards
+    for r in res:
+        assert r[3] == 2.0 and r[4] == 1.0                                # max over ranks
+        assert r[5] == pytest.approx(1000 * 2 * 10 / 2.0)                 # all ranks' env-steps / slowest
