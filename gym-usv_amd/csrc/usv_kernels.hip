@@ -69,6 +69,26 @@ constexpr int kEPBReset = 64;   // envs per block of the reset kernel
 constexpr int kLidDefault = 7;  // lidar variant of the reset kernel (all variants give identical scans)
 
 template <typename R> __device__ __forceinline__ R big() { return R(1e30); }
+
+// Diagnostic build only (-DUSV_DIAG_STAMPS): per-block s_memrealtime (100 MHz) stamps at the
+// phase boundaries of the step kernel, read back with usv_diag_stamps().  Never in the product.
+#ifdef USV_DIAG_STAMPS
+constexpr int kStampSlots = 8;
+__device__ unsigned long long g_stamps[32768 * kStampSlots];
+#define USV_STAMP(i)                                                                      \
+  do {                                                                                    \
+    if (threadIdx.x == 0 && blockIdx.x < 32768)                                           \
+      g_stamps[blockIdx.x * kStampSlots + (i)] = __builtin_amdgcn_s_memrealtime();        \
+  } while (0)
+#define USV_STAMP_W(i)                                                                    \
+  do {                                                                                    \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 32768)                                    \
+      g_stamps[blockIdx.x * kStampSlots + (i)] = __builtin_amdgcn_s_memrealtime();        \
+  } while (0)
+#else
+#define USV_STAMP(i) do {} while (0)
+#define USV_STAMP_W(i) do {} while (0)
+#endif
 template <typename R> struct Vec2;
 template <> struct Vec2<float> { using T = float2; };
 template <> struct Vec2<double> { using T = double2; };
@@ -535,6 +555,7 @@ __global__ __launch_bounds__(kBlock) void step_kernel(State<R> S, IO<R> io) {
   const int ne = S.N - e0 < EPB ? S.N - e0 : EPB;   // envs of this block
   const int cap = S.cap;
 
+  USV_STAMP(0);
   lds_prologue(S, lds, tid);
   if (tid < kWave) {
     // ---- phase 1 (wave 0): lane-per-env dynamics
@@ -557,6 +578,7 @@ __global__ __launch_bounds__(kBlock) void step_kernel(State<R> S, IO<R> io) {
       sh.trunc[tid] = trunc;
       sh.n[tid] = S.n_obs[e];
     }
+    USV_STAMP(1);
   } else {
     // ---- phase 1 (waves 1..3): stage this block's obstacle rows in LDS meanwhile
     // rows k = wave-1, wave+2, ...; four loads in flight before their LDS stores
@@ -578,6 +600,7 @@ __global__ __launch_bounds__(kBlock) void step_kernel(State<R> S, IO<R> io) {
     }
   }
   __syncthreads();
+  USV_STAMP(2);
 
   // ---- phase 2: wave-per-env lidar + observation rows
   unsigned long long* wslot = slots + wave * 128;
@@ -611,12 +634,15 @@ __global__ __launch_bounds__(kBlock) void step_kernel(State<R> S, IO<R> io) {
       S.sensor_last[(size_t)e * kSensors + 64 + l] = sc.rd1;
     }
   }
+  if (wave == 0) USV_STAMP(3);
   // same-step autoreset of this wave's done envs (own loop: keeps the lidar loop's registers free)
   if (S.autoreset == USV_AUTORESET_SAME_STEP) {
     for (int k = wave; k < ne; k += kWaves)
       if (sh.term[k] | sh.trunc[k]) reset_wave<R, MODE>(S, e0 + k, io.obs + (size_t)(e0 + k) * kObsDim);
   }
+  if (wave == 0) USV_STAMP(4);
   __syncthreads();
+  USV_STAMP(5);
 
   // ---- phase 3: lane-per-env reward and flags (coalesced)
   if (tid < ne) {
@@ -627,6 +653,7 @@ __global__ __launch_bounds__(kBlock) void step_kernel(State<R> S, IO<R> io) {
     io.term[e] = term;
     io.trunc[e] = trunc;
   }
+  USV_STAMP(6);
 }
 
 // --------------------------------------------------------------------------- reset kernel
@@ -907,6 +934,14 @@ Handle* as_handle(void* p) { return static_cast<Handle*>(p); }
 extern "C" {
 
 int usv_abi_version(void) { return USV_ABI_VERSION; }
+
+#ifdef USV_DIAG_STAMPS
+int usv_diag_stamps(void* host, size_t bytes) {
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), bytes < sizeof(g_stamps) ? bytes : sizeof(g_stamps)));
+  return USV_OK;
+}
+#endif
 
 const char* usv_last_error(void) { return g_err.c_str(); }
 
