@@ -38,19 +38,22 @@ enum RealField {
   F_PX0, F_PY0, F_PX1, F_PY1, F_MAX_U, F_MAX_R, F_REF_V, F_NREAL
 };
 
+// Device state.  All real SoA fields share one allocation (field i at freal + i*fstride) and
+// the int fields another, so the kernel holds two base pointers instead of twenty (kernel
+// arguments live in SGPRs; fewer of them keeps the kernel at <= 80 SGPRs = 8 blocks per CU).
+enum IntField { I_NOBS, I_ELAPSED, I_EPISODE, I_SCAN, I_NINT };
 template <typename R> struct State {
-  R* f[F_NREAL];           // [field][N]
-  int32_t* n_obs;          // [N]
-  int32_t* elapsed;        // [N]
-  int32_t* episode;        // [N]
-  int32_t* scan_valid;     // [N]
+  R* freal;                // [F_NREAL][fstride]
+  int32_t* fint;           // [I_NINT][fstride]
   R4<R>* obst;             // [N][cap] (x, y, r, r*r)
   R* sensor_last;          // [N][128]
   R* asmc;                 // [16][N]
-  const R* ray_co;         // [128] cos(start + i*res)
-  const R* ray_so;         // [128] sin(start + i*res)
+  const R* ray_tab;        // [2][128] cos / sin(start + i*res)
   int N, cap, limit, autoreset;
+  int fstride;             // elements between fields (>= N, 256-B aligned)
   uint64_t seed, gid0;
+  __host__ __device__ R* F(int i) const { return freal + (size_t)i * fstride; }
+  __host__ __device__ int32_t* I(int i) const { return fint + (size_t)i * fstride; }
 };
 
 template <typename R> struct IO {
@@ -149,7 +152,7 @@ __device__ __forceinline__ void philox_uniforms(Philox& g, int l, Uni4<double>& 
 template <typename R, int MODE>
 __device__ __forceinline__ void reset_wave(const State<R>& S, int e, float* row) {
   const int l = lane_id();
-  const int ep = uniform(S.episode[e]);
+  const int ep = uniform(S.I(I_EPISODE)[e]);
   Philox g(S.seed, S.gid0 + (uint64_t)e, (uint32_t)ep);
   Uni4<R> U;
   philox_uniforms(g, l, U);
@@ -191,16 +194,16 @@ __device__ __forceinline__ void reset_wave(const State<R>& S, int e, float* row)
     const R refv = R(0.75) + (mu - R(0.75)) * bcast(U.u[0], 35);
     R sa, ca;
     m_sincos(ang, &sa, &ca);
-    S.f[F_X][e] = sx; S.f[F_Y][e] = sy; S.f[F_PSI][e] = psi;
-    S.f[F_U][e] = u; S.f[F_V][e] = v; S.f[F_R][e] = r;
-    S.f[F_PROGRESS][e] = R(0);
-    S.f[F_PX0][e] = sx; S.f[F_PY0][e] = sy;
-    S.f[F_PX1][e] = sx + ca * dist; S.f[F_PY1][e] = sy + sa * dist;                // :243
-    S.f[F_MAX_U][e] = mu; S.f[F_MAX_R][e] = mr; S.f[F_REF_V][e] = refv;
-    S.n_obs[e] = cnt;
-    S.elapsed[e] = 0;
-    S.episode[e] = ep + 1;
-    S.scan_valid[e] = 0;
+    S.F(F_X)[e] = sx; S.F(F_Y)[e] = sy; S.F(F_PSI)[e] = psi;
+    S.F(F_U)[e] = u; S.F(F_V)[e] = v; S.F(F_R)[e] = r;
+    S.F(F_PROGRESS)[e] = R(0);
+    S.F(F_PX0)[e] = sx; S.F(F_PY0)[e] = sy;
+    S.F(F_PX1)[e] = sx + ca * dist; S.F(F_PY1)[e] = sy + sa * dist;                // :243
+    S.F(F_MAX_U)[e] = mu; S.F(F_MAX_R)[e] = mr; S.F(F_REF_V)[e] = refv;
+    S.I(I_NOBS)[e] = cnt;
+    S.I(I_ELAPSED)[e] = 0;
+    S.I(I_EPISODE)[e] = ep + 1;
+    S.I(I_SCAN)[e] = 0;
     // reset obs: _get_obs(zeros(3)) with the random target_position (:302, :72-80); position
     // == path_start, so ye == 0 exactly
     const R angle = wrap_angle(m_atan2(ty - sy, tx - sx) - psi);
@@ -219,8 +222,8 @@ __device__ __forceinline__ void reset_wave(const State<R>& S, int e, float* row)
 template <typename R, int MODE>
 __device__ void env_dynamics(const State<R>& S, int e, float a_u, float a_r, float (&hdr)[kHdr],
                              R& px, R& py, R& psp, R& pcp, R& partial, bool& trunc) {
-  R x = S.f[F_X][e], y = S.f[F_Y][e], psi = S.f[F_PSI][e];
-  R u = S.f[F_U][e], v = S.f[F_V][e], r = S.f[F_R][e];
+  R x = S.F(F_X)[e], y = S.F(F_Y)[e], psi = S.F(F_PSI)[e];
+  R u = S.F(F_U)[e], v = S.F(F_V)[e], r = S.F(F_R)[e];
   if (MODE == USV_MODE_ASMC_SIMPLE) {
     R s[kAsmcN];
 #pragma unroll
@@ -232,8 +235,8 @@ __device__ void env_dynamics(const State<R>& S, int e, float a_u, float a_r, flo
     a_u = 0.0f;                                                                   // step(zeros(2))
     a_r = 0.0f;
   }
-  const R lu = S.f[F_LAST_U][e], lr = S.f[F_LAST_R][e];
-  const R mu = S.f[F_MAX_U][e], mr = S.f[F_MAX_R][e], refv = S.f[F_REF_V][e];
+  const R lu = S.F(F_LAST_U)[e], lr = S.F(F_LAST_R)[e];
+  const R mu = S.F(F_MAX_U)[e], mr = S.F(F_MAX_R)[e], refv = S.F(F_REF_V)[e];
   // action = max_action * insert(action, 1, 0); filtered 0.8/0.2 (:311-317)
   const R a3u = R(0.8) * lu + R(0.2) * (mu * R(a_u));
   const R a3r = R(0.8) * lr + R(0.2) * (mr * R(a_r));
@@ -249,11 +252,11 @@ __device__ void env_dynamics(const State<R>& S, int e, float a_u, float a_r, flo
   y = y + (u * sp) * R(kDt);
   psi = psi + r * R(kDt);
   // _get_closest_point (:139-148)
-  const R x0 = S.f[F_PX0][e], y0 = S.f[F_PY0][e];
-  const R dx = S.f[F_PX1][e] - x0, dy = S.f[F_PY1][e] - y0;
+  const R x0 = S.F(F_PX0)[e], y0 = S.F(F_PY0)[e];
+  const R dx = S.F(F_PX1)[e] - x0, dy = S.F(F_PY1)[e] - y0;
   R a = (dy * (y - y0) + dx * (x - x0)) / (dx * dx + dy * dy);
   a = a + R(kLookahead);
-  a = m_clip(a, S.f[F_PROGRESS][e], R(1));
+  a = m_clip(a, S.F(F_PROGRESS)[e], R(1));
   const R tx = x0 + a * dx, ty = y0 + a * dy;
   // _get_ye (:133-137), _get_angle_to_target (:67-69), distance (:74)
   const R ak = m_atan2(dy, dx);
@@ -262,7 +265,7 @@ __device__ void env_dynamics(const State<R>& S, int e, float a_u, float a_r, flo
   const R ye = -(x - x0) * sak + (y - y0) * cak;
   const R angle = wrap_angle(m_atan2(ty - y, tx - x) - psi);
   const R dist = m_hypot(x - tx, y - ty);
-  const int el = S.elapsed[e] + 1;
+  const int el = S.I(I_ELAPSED)[e] + 1;
   trunc = (x > R(kBound)) | (x < R(0)) | (y > R(kBound)) | (y < R(0)) |   // :336
           (S.limit > 0 && el >= S.limit);                                 // TimeLimit
   make_header<R>(hdr, u, v, r, angle, dist, ye, refv, lu, lr, mu, mr);   // obs uses PREVIOUS action
@@ -275,12 +278,12 @@ __device__ void env_dynamics(const State<R>& S, int e, float a_u, float a_r, flo
   const R vel_r = m_exp(-m_abs(m_hypot(u, v) - refv)) * R(0.05);
   const R dact_r = -(dact / R(2)) * R(0.15);
   partial = ye_r + ang_r + vel_r + dact_r;
-  S.f[F_X][e] = x; S.f[F_Y][e] = y; S.f[F_PSI][e] = psi;
-  S.f[F_U][e] = u; S.f[F_V][e] = v; S.f[F_R][e] = r;
-  S.f[F_LAST_U][e] = a3u; S.f[F_LAST_R][e] = a3r;
-  S.f[F_PROGRESS][e] = a;
-  S.elapsed[e] = el;
-  S.scan_valid[e] = 1;
+  S.F(F_X)[e] = x; S.F(F_Y)[e] = y; S.F(F_PSI)[e] = psi;
+  S.F(F_U)[e] = u; S.F(F_V)[e] = v; S.F(F_R)[e] = r;
+  S.F(F_LAST_U)[e] = a3u; S.F(F_LAST_R)[e] = a3r;
+  S.F(F_PROGRESS)[e] = a;
+  S.I(I_ELAPSED)[e] = el;
+  S.I(I_SCAN)[e] = 1;
   px = x; py = y;
   m_sincos(psi, &psp, &pcp);
 }
@@ -431,14 +434,37 @@ __device__ __forceinline__ void lidar_brute(R dx, R dy, R r2, R key, R d, R rr, 
 }
 
 // Angular-window lidar (f32).  Lane j computes the ray-index windows its obstacle can touch
-// (conservative: +1.5 rays of margin around asin(r/d), pi/2 when the boat is inside it), the
-// (obstacle, ray) pairs are expanded over the lanes (prefix sum + per-lane binary search), each
-// pair runs the same exact test as the brute loop, and the hit with the smallest
-// (key, index) per ray wins through an LDS ds_min_u64 -- the min-key rule, bit-identical to
-// lidar_brute.  ~100 pair tests per env instead of 128 x n.
-__device__ __forceinline__ void lidar_window(float dx, float dy, float r2, float key, float d, float rr,
-                                             bool valid, int n, float sp, float cp, const float2* rayoff,
-                                             unsigned long long* slot, Scan<float>& out) {
+// (conservative: 1.5 rays of margin around an upper bound of asin(r/d), pi/2 when the boat is
+// inside it), the (obstacle, ray) pairs are expanded over the lanes (prefix sum; each pair's
+// owner found with LDS start markers and a max-scan), each pair runs the same exact test as
+// the brute loop, and the hit with the smallest (key, index) per ray wins through an LDS
+// ds_min_u64 -- the min-key rule, bit-identical to lidar_brute.  ~100 pair tests per env
+// instead of 128 x n.
+struct WinLds {
+  unsigned long long* slot;   // [128] per wave, ~0 between envs
+  int* mark;                  // [64]  per wave
+  const float2* rayoff;       // [128] block-shared ray offset table
+  const float* lx;            // this env's obstacle row (LDS SoA)
+  const float* ly;
+  const float* lr;
+};
+
+// Inclusive max-scan over the 64 lanes (DPP row scans + row carries); identity -1.
+__device__ __forceinline__ int wave_incl_max(int v) {
+  v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x111, 0xF, 0xF, false));   // row_shr:1
+  v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x112, 0xF, 0xF, false));   // row_shr:2
+  v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x114, 0xF, 0xF, false));   // row_shr:4
+  v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x118, 0xF, 0xF, false));   // row_shr:8
+  const int l = lane_id();
+  const int t0 = __builtin_amdgcn_readlane(v, 15);
+  const int t1 = max(t0, __builtin_amdgcn_readlane(v, 31));
+  const int t2 = max(t1, __builtin_amdgcn_readlane(v, 47));
+  return max(v, l >= 48 ? t2 : l >= 32 ? t1 : l >= 16 ? t0 : -1);
+}
+
+__device__ __forceinline__ void lidar_window(float dx, float dy, float key, float d, float rr, bool valid,
+                                             float px, float py, float sp, float cp, const WinLds& L,
+                                             Scan<float>& out) {
   const int l = lane_id();
   const float c0r = ray_c(cp, sp, (float)kStartC, (float)kStartS);
   const float s0r = ray_s(cp, sp, (float)kStartC, (float)kStartS);
@@ -446,8 +472,10 @@ __device__ __forceinline__ void lidar_window(float dx, float dy, float r2, float
   const float phi = fast_atan2(b, a);                 // CCW angle from ray 0; ray i at i*res
   const float margin = (float)(1.5 * kRes);
   const bool inside = d <= rr * 1.001f;
+  // asin(x) <= x + (pi/2 - 1) x^3 on [0, 1] (Taylor coefficients >= 0 summing to pi/2 at x = 1)
+  const float x = fminf(rr * __builtin_amdgcn_rcpf(d), 1.0f);
   const float half = inside ? (float)(kPi / 2) + margin
-                            : fast_atan2(rr, __builtin_amdgcn_sqrtf(fmaxf(d * d - rr * rr, 0.0f))) + margin;
+                            : fmaf((float)(kPi / 2 - 1) * x, x * x, x) + margin;
   const float inv = (float)(1.0 / kRes);
   const int lo1 = max(0, (int)ceilf((phi - half) * inv)), hi1 = min(127, (int)floorf((phi + half) * inv));
   const float phi2 = phi + (float)(2 * kPi);
@@ -457,57 +485,73 @@ __device__ __forceinline__ void lidar_window(float dx, float dy, float r2, float
   const int incl = wave_incl_scan(cnt);
   const int off = incl - cnt;
   const int W = __builtin_amdgcn_readlane(incl, 63);
-  const int off_s = valid ? off : (1 << 24);          // lanes without an obstacle are never owners
   const int meta = lo1 | (len1 << 8) | (lo2 << 16);
   const unsigned ok = ord_key(key);
+  int carry = -1;
   for (int base = 0; base < W; base += kWave) {       // wave-uniform pass count
+    // owner of pair q = base + l: the obstacle whose run of pairs starts at or before q
+    L.mark[l] = -1;
+    if (cnt > 0 && off >= base && off < base + kWave) L.mark[off - base] = l;
+    const int j = max(wave_incl_max(L.mark[l]), carry);
+    carry = __builtin_amdgcn_readlane(j, 63);
     const int q = base + l;
-    int j = 0;
-#pragma unroll
-    for (int step = 32; step >= 1; step >>= 1) {      // largest j with off_j <= q
-      const int cand = j + step;
-      const int ov = __shfl(off_s, cand & 63, kWave);
-      j = (cand < kWave && ov <= q) ? cand : j;
-    }
-    const int k = q - __shfl(off, j, kWave);
-    const int mj = __shfl(meta, j, kWave);
+    const int jj = j < 0 ? 0 : j;
+    const int k = q - __shfl(off, jj, kWave);
+    const int mj = __shfl(meta, jj, kWave);
+    const unsigned gk = (unsigned)__shfl((int)ok, jj, kWave);
     const int l1 = mj & 255, n1 = (mj >> 8) & 255, l2 = mj >> 16;
     int i = k < n1 ? l1 + k : l2 + (k - n1);
     i = min(max(i, 0), 127);
-    const float gdx = __shfl(dx, j, kWave), gdy = __shfl(dy, j, kWave), gr2 = __shfl(r2, j, kWave);
-    const unsigned gk = (unsigned)__shfl((int)ok, j, kWave);
-    const float2 cs = rayoff[i];
+    const float gdx = L.lx[jj] - px, gdy = L.ly[jj] - py, gr = L.lr[jj];
+    const float2 cs = L.rayoff[i];
     const float c = ray_c(cp, sp, cs.x, cs.y), s = ray_s(cp, sp, cs.x, cs.y);
     const float proj = fmaf(gdx, c, gdy * s);
     const float perp = fmaf(gdx, s, -(gdy * c));
-    const float delta = fmaf(-perp, perp, gr2);
+    const float delta = fmaf(-perp, perp, gr * gr);
     if ((q < W) & (proj >= 0.0f) & (delta >= 0.0f))
-      atomicMin(&slot[i], ((unsigned long long)gk << 32) | (unsigned)j);
+      atomicMin(&L.slot[i], ((unsigned long long)gk << 32) | (unsigned)jj);
   }
-  const unsigned long long v0 = slot[l], v1 = slot[l + 64];
-  slot[l] = ~0ull;                                    // re-arm for this wave's next env
-  slot[l + 64] = ~0ull;
-  const float2 cs0 = rayoff[l], cs1 = rayoff[l + 64];
-  const int j0 = v0 == ~0ull ? -1 : (int)(unsigned)v0, j1 = v1 == ~0ull ? -1 : (int)(unsigned)v1;
-  out.rd0 = reading_of(ray_c(cp, sp, cs0.x, cs0.y), ray_s(cp, sp, cs0.x, cs0.y), j0, dx, dy, r2);
-  out.rd1 = reading_of(ray_c(cp, sp, cs1.x, cs1.y), ray_s(cp, sp, cs1.x, cs1.y), j1, dx, dy, r2);
-  (void)n;
+  const unsigned long long v0 = L.slot[l], v1 = L.slot[l + 64];
+  L.slot[l] = ~0ull;                                  // re-arm for this wave's next env
+  L.slot[l + 64] = ~0ull;
+  const int j0 = (int)(unsigned)v0 & 63, j1 = (int)(unsigned)v1 & 63;
+  const float2 cs0 = L.rayoff[l], cs1 = L.rayoff[l + 64];
+  {
+    const float c = ray_c(cp, sp, cs0.x, cs0.y), s = ray_s(cp, sp, cs0.x, cs0.y);
+    const float gdx = L.lx[j0] - px, gdy = L.ly[j0] - py, gr = L.lr[j0];
+    const float proj = fmaf(gdx, c, gdy * s), perp = fmaf(gdx, s, -(gdy * c));
+    out.rd0 = v0 != ~0ull ? proj - l_sqrt(fmaf(-perp, perp, gr * gr)) : (float)kSensorMax;
+  }
+  {
+    const float c = ray_c(cp, sp, cs1.x, cs1.y), s = ray_s(cp, sp, cs1.x, cs1.y);
+    const float gdx = L.lx[j1] - px, gdy = L.ly[j1] - py, gr = L.lr[j1];
+    const float proj = fmaf(gdx, c, gdy * s), perp = fmaf(gdx, s, -(gdy * c));
+    out.rd1 = v1 != ~0ull ? proj - l_sqrt(fmaf(-perp, perp, gr * gr)) : (float)kSensorMax;
+  }
 }
 
+// Obstacle row of one env in LDS (SoA), plus the block-shared tables.
+template <typename R> struct EnvLds {
+  const R* lx;
+  const R* ly;
+  const R* lr;
+};
+
 template <typename R, int LID>
-__device__ __forceinline__ void lidar_wave(const R4<R>& o, int n, R px, R py, R sp, R cp,
+__device__ __forceinline__ void lidar_wave(const EnvLds<R>& E, int n, R px, R py, R sp, R cp,
                                            const typename Vec2<R>::T* rayoff, unsigned long long* slot,
-                                           Scan<R>& out) {
+                                           int* mark, Scan<R>& out) {
   const int l = lane_id();
   const bool valid = l < n;
-  const R dx = o.x - px, dy = o.y - py, r2 = o.w, rr = o.z;
+  const R ox = valid ? E.lx[l] : R(0), oy = valid ? E.ly[l] : R(0), rr = valid ? E.lr[l] : R(0);
+  const R dx = ox - px, dy = oy - py, r2 = rr * rr;
   const R d = l_sqrt(m_fma(dx, dx, dy * dy));
   const R key = valid ? d - rr : big<R>();                                      // simple_env.py:205-206
   out.term = __ballot(valid & (key < R(kTermDist))) != 0;                       // :334
   out.far = __ballot(valid & (d >= R(0.99 * kSensorMax))) != 0;
   if constexpr (std::is_same<R, float>::value && (LID & kLidWindow) != 0) {
     if (!out.far) {
-      lidar_window(dx, dy, r2, key, d, rr, valid, n, sp, cp, rayoff, slot, out);
+      lidar_window(dx, dy, key, d, rr, valid, px, py, sp, cp, WinLds{slot, mark, rayoff, E.lx, E.ly, E.lr}, out);
       return;
     }
   }
@@ -517,18 +561,22 @@ __device__ __forceinline__ void lidar_wave(const R4<R>& o, int n, R px, R py, R 
 }
 
 template <typename R, int EPB> struct alignas(16) Scratch {
-  float hdr[kHdr][EPB + 1];
   R px[EPB], py[EPB], sp[EPB], cp[EPB], partial[EPB];
   int n[EPB];
   uint8_t trunc[EPB], term[EPB], coll[EPB];
 };
 
-// Dynamic LDS carve: [ray offset table 128 x Vec2][per-wave pair slots 4 x 128 x u64]
-//                    [obstacle rows EPB x cap x R4]
+// Dynamic LDS carve (16-B aligned pieces):
+//   [ray offset table 128 x Vec2][pair slots 4 waves x 128 x u64][owner marks 4 x 64 x i32]
+//   [obstacle rows: x[EPB][cap], y[EPB][cap], r[EPB][cap]]
 template <typename R> __host__ __device__ constexpr size_t lds_rayoff_bytes() { return 128 * 2 * sizeof(R); }
 constexpr size_t kLdsSlotBytes = (size_t)kWaves * 128 * 8;
+constexpr size_t kLdsMarkBytes = (size_t)kWaves * 64 * 4;
+template <typename R> __host__ __device__ constexpr size_t lds_head_bytes() {
+  return lds_rayoff_bytes<R>() + kLdsSlotBytes + kLdsMarkBytes;
+}
 template <typename R> __host__ __device__ size_t lds_bytes(int epb, int cap) {
-  return lds_rayoff_bytes<R>() + kLdsSlotBytes + (size_t)epb * cap * sizeof(R4<R>);
+  return lds_head_bytes<R>() + 3 * (((size_t)epb * cap * sizeof(R) + 15) & ~(size_t)15);
 }
 
 // Block prologue shared by the step and reset kernels: ray-offset table and slot init.
@@ -536,29 +584,33 @@ template <typename R>
 __device__ __forceinline__ void lds_prologue(const State<R>& S, char* lds, int tid) {
   auto* rayoff = reinterpret_cast<typename Vec2<R>::T*>(lds);
   auto* slots = reinterpret_cast<unsigned long long*>(lds + lds_rayoff_bytes<R>());
-  if (tid < kSensors) rayoff[tid] = typename Vec2<R>::T{S.ray_co[tid], S.ray_so[tid]};
+  if (tid < kSensors) rayoff[tid] = typename Vec2<R>::T{S.ray_tab[tid], S.ray_tab[kSensors + tid]};
   for (int i = tid; i < kWaves * 128; i += kBlock) slots[i] = ~0ull;
 }
 
 // --------------------------------------------------------------------------- step kernel
 template <typename R, int MODE, int EPB, int LID>
-__global__ __launch_bounds__(kBlock) void step_kernel(State<R> S, IO<R> io) {
+__device__ __forceinline__ void step_body(const State<R>& S, const IO<R>& io) {
   __shared__ Scratch<R, EPB> sh;
   extern __shared__ __attribute__((aligned(16))) char lds[];
   auto* rayoff = reinterpret_cast<typename Vec2<R>::T*>(lds);
   auto* slots = reinterpret_cast<unsigned long long*>(lds + lds_rayoff_bytes<R>());
-  R4<R>* lobst = reinterpret_cast<R4<R>*>(lds + lds_rayoff_bytes<R>() + kLdsSlotBytes);
+  int* marks = reinterpret_cast<int*>(lds + lds_rayoff_bytes<R>() + kLdsSlotBytes);
   const int tid = threadIdx.x;
   const int wave = tid / kWave;
   const int l = lane_id();
   const int e0 = blockIdx.x * EPB;
   const int ne = S.N - e0 < EPB ? S.N - e0 : EPB;   // envs of this block
   const int cap = S.cap;
+  const size_t plane = (((size_t)EPB * cap * sizeof(R) + 15) & ~(size_t)15) / sizeof(R);
+  R* lox = reinterpret_cast<R*>(lds + lds_head_bytes<R>());
+  R* loy = lox + plane;
+  R* lor = loy + plane;
 
   USV_STAMP(0);
   lds_prologue(S, lds, tid);
   if (tid < kWave) {
-    // ---- phase 1 (wave 0): lane-per-env dynamics
+    // ---- phase 1 (wave 0): lane-per-env dynamics; the obs header goes straight to the row
     if (tid < ne) {
       const int e = e0 + tid;
       const float2 a = reinterpret_cast<const float2*>(io.act)[e];
@@ -566,21 +618,22 @@ __global__ __launch_bounds__(kBlock) void step_kernel(State<R> S, IO<R> io) {
       R px, py, sp, cp, partial;
       bool trunc;
 #ifdef USV_DIAG_NODYN
-      px = S.f[F_X][e] + a.x; py = S.f[F_Y][e] + a.y; sp = R(0.5); cp = R(0.8); partial = R(0); trunc = false;
+      px = S.F(F_X)[e] + a.x; py = S.F(F_Y)[e] + a.y; sp = R(0.5); cp = R(0.8); partial = R(0); trunc = false;
       for (int i = 0; i < kHdr; ++i) hdr[i] = (float)px;
 #else
       env_dynamics<R, MODE>(S, e, a.x, a.y, hdr, px, py, sp, cp, partial, trunc);
 #endif
+      float* row = io.obs + (size_t)e * kObsDim;
 #pragma unroll
-      for (int i = 0; i < kHdr; ++i) sh.hdr[i][tid] = hdr[i];
+      for (int i = 0; i < kHdr; ++i) row[i] = hdr[i];
       sh.px[tid] = px; sh.py[tid] = py; sh.sp[tid] = sp; sh.cp[tid] = cp;
       sh.partial[tid] = partial;
       sh.trunc[tid] = trunc;
-      sh.n[tid] = S.n_obs[e];
+      sh.n[tid] = S.I(I_NOBS)[e];
     }
     USV_STAMP(1);
   } else {
-    // ---- phase 1 (waves 1..3): stage this block's obstacle rows in LDS meanwhile
+    // ---- phase 1 (waves 1..3): stage this block's obstacle rows in LDS (SoA) meanwhile;
     // rows k = wave-1, wave+2, ...; four loads in flight before their LDS stores
     const R4<R>* src = S.obst + (size_t)e0 * cap + l;
     const R4<R> z{R(0), R(0), R(0), R(0)};
@@ -592,10 +645,10 @@ __global__ __launch_bounds__(kBlock) void step_kernel(State<R> S, IO<R> io) {
       const R4<R> b2 = lane_ok && k2 < ne ? src[(size_t)k2 * cap] : z;
       const R4<R> b3 = lane_ok && k3 < ne ? src[(size_t)k3 * cap] : z;
       if (lane_ok) {
-        lobst[k * cap + l] = b0;
-        if (k1 < ne) lobst[k1 * cap + l] = b1;
-        if (k2 < ne) lobst[k2 * cap + l] = b2;
-        if (k3 < ne) lobst[k3 * cap + l] = b3;
+        lox[k * cap + l] = b0.x; loy[k * cap + l] = b0.y; lor[k * cap + l] = b0.z;
+        if (k1 < ne) { lox[k1 * cap + l] = b1.x; loy[k1 * cap + l] = b1.y; lor[k1 * cap + l] = b1.z; }
+        if (k2 < ne) { lox[k2 * cap + l] = b2.x; loy[k2 * cap + l] = b2.y; lor[k2 * cap + l] = b2.z; }
+        if (k3 < ne) { lox[k3 * cap + l] = b3.x; loy[k3 * cap + l] = b3.y; lor[k3 * cap + l] = b3.z; }
       }
     }
   }
@@ -604,15 +657,16 @@ __global__ __launch_bounds__(kBlock) void step_kernel(State<R> S, IO<R> io) {
 
   // ---- phase 2: wave-per-env lidar + observation rows
   unsigned long long* wslot = slots + wave * 128;
+  int* wmark = marks + wave * 64;
   for (int k = wave; k < ne; k += kWaves) {
     const int e = e0 + k;
     const int n = uniform(sh.n[k]);
-    const R4<R> o = l < n ? lobst[k * cap + l] : R4<R>{R(0), R(0), R(0), R(0)};
     Scan<R> sc;
 #ifdef USV_DIAG_NOLIDAR
-    sc.rd0 = sc.rd1 = R(kSensorMax) + o.x; sc.term = false; sc.far = false;
+    sc.rd0 = sc.rd1 = R(kSensorMax) + lox[k * cap]; sc.term = false; sc.far = false;
 #else
-    lidar_wave<R, LID>(o, n, sh.px[k], sh.py[k], sh.sp[k], sh.cp[k], rayoff, wslot, sc);
+    lidar_wave<R, LID>(EnvLds<R>{lox + k * cap, loy + k * cap, lor + k * cap}, n, sh.px[k], sh.py[k],
+                       sh.sp[k], sh.cp[k], rayoff, wslot, wmark, sc);
 #endif
     const bool done = sc.term || sh.trunc[k];
     const bool coll = __ballot((sc.rd0 < R(kCollDist)) | (sc.rd1 < R(kCollDist))) != 0;  // :153-156
@@ -622,12 +676,11 @@ __global__ __launch_bounds__(kBlock) void step_kernel(State<R> S, IO<R> io) {
     float* row = io.obs + (size_t)e * kObsDim;
     row[kHdr + l] = s0;                                        // stale scan is kept by reset
     row[kHdr + 64 + l] = s1;
-    if (!reset_now && l < kHdr) row[l] = sh.hdr[l][k];
-    if (done && io.fobs) {
+    if (done && io.fobs) {                                     // terminal obs (header from phase 1)
       float* f = io.fobs + (size_t)e * kObsDim;
       f[kHdr + l] = s0;
       f[kHdr + 64 + l] = s1;
-      if (l < kHdr) f[l] = sh.hdr[l][k];
+      if (l < kHdr) f[l] = row[l];
     }
     if (reset_now) {
       S.sensor_last[(size_t)e * kSensors + l] = sc.rd0;
@@ -656,6 +709,19 @@ __global__ __launch_bounds__(kBlock) void step_kernel(State<R> S, IO<R> io) {
   USV_STAMP(6);
 }
 
+// 8 blocks of 256 threads per CU need <= 64 VGPRs and .sgpr_count <= 80 (MI355X_MICROARCH.md,
+// residency: 800 / (ceil(sgpr/16)*16 + 16) blocks; the occupancy API over-reports in 81..96).
+// The f32 usv-simple body fits; the ASMC and f64 bodies need more registers and run at the
+// occupancy their register use allows.
+template <typename R, int MODE, int EPB, int LID>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(80), amdgpu_num_vgpr(64)))
+void step_kernel_tight(State<R> S, IO<R> io) { step_body<R, MODE, EPB, LID>(S, io); }
+
+template <typename R, int MODE, int EPB, int LID>
+__global__ __launch_bounds__(kBlock) void step_kernel(State<R> S, IO<R> io) {
+  step_body<R, MODE, EPB, LID>(S, io);
+}
+
 // --------------------------------------------------------------------------- reset kernel
 // Explicit (host-requested) reset of masked envs.  Reset obs = new header + the stale
 // sensor_data: the scan at the last stepped pose (recomputed when that pose is still the
@@ -670,6 +736,11 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(State<R> S, IO<R> io) {
   const int l = lane_id();
   const int e0 = blockIdx.x * kEPBReset;
   const int ne = S.N - e0 < kEPBReset ? S.N - e0 : kEPBReset;
+  int* marks = reinterpret_cast<int*>(lds + lds_rayoff_bytes<R>() + kLdsSlotBytes);
+  // one obstacle row per wave (SoA) in the obstacle area
+  R* wx = reinterpret_cast<R*>(lds + lds_head_bytes<R>()) + wave * 3 * 64;
+  R* wy = wx + 64;
+  R* wr = wy + 64;
   lds_prologue(S, lds, tid);
   __syncthreads();
   for (int k = wave; k < ne; k += kWaves) {
@@ -677,13 +748,17 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(State<R> S, IO<R> io) {
     if (io.mask && !io.mask[e]) continue;
     R rd0, rd1;
     R* last = S.sensor_last + (size_t)e * kSensors;
-    if (S.scan_valid[e]) {
+    if (S.I(I_SCAN)[e]) {
       R sp, cp;
-      m_sincos(S.f[F_PSI][e], &sp, &cp);
-      const int n = uniform(S.n_obs[e]);
-      const R4<R> o = l < n ? S.obst[(size_t)e * S.cap + l] : R4<R>{R(0), R(0), R(0), R(0)};
+      m_sincos(S.F(F_PSI)[e], &sp, &cp);
+      const int n = uniform(S.I(I_NOBS)[e]);
+      if (l < S.cap) {
+        const R4<R> o = S.obst[(size_t)e * S.cap + l];
+        wx[l] = o.x; wy[l] = o.y; wr[l] = o.z;
+      }
       Scan<R> sc;
-      lidar_wave<R, kLidDefault>(o, n, S.f[F_X][e], S.f[F_Y][e], sp, cp, rayoff, slots + wave * 128, sc);
+      lidar_wave<R, kLidDefault>(EnvLds<R>{wx, wy, wr}, n, S.F(F_X)[e], S.F(F_Y)[e], sp, cp, rayoff,
+                                 slots + wave * 128, marks + wave * 64, sc);
       rd0 = sc.rd0;
       rd1 = sc.rd1;
       last[l] = rd0;
@@ -752,25 +827,22 @@ template <typename R>
 int carve(Handle* h, State<R>& S) {
   const size_t N = (size_t)h->cfg.num_envs, cap = (size_t)h->cfg.obstacle_cap;
   auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
-  const size_t bytes = F_NREAL * al(N * sizeof(R)) + 4 * al(N * 4) + al(N * cap * sizeof(R4<R>)) +
-                       al(N * kSensors * sizeof(R)) + al((size_t)kAsmcN * N * sizeof(R)) +
-                       2 * al(kSensors * sizeof(R));
+  const size_t stride = al(N * sizeof(R)) / sizeof(R);   // also >= N int32 (sizeof(R) >= 4)
+  const size_t bytes = F_NREAL * stride * sizeof(R) + al(I_NINT * stride * 4) +
+                       al(N * cap * sizeof(R4<R>)) + al(N * kSensors * sizeof(R)) +
+                       al((size_t)kAsmcN * N * sizeof(R)) + al(2 * kSensors * sizeof(R));
   HIP_TRY(hipMalloc(&h->slab, bytes));
   HIP_TRY(hipMemset(h->slab, 0, bytes));
   char* p = (char*)h->slab;
   auto take = [&](size_t b) { char* q = p; p += al(b); return (void*)q; };
-  for (int i = 0; i < F_NREAL; ++i) S.f[i] = (R*)take(N * sizeof(R));
-  S.n_obs = (int32_t*)take(N * 4);
-  S.elapsed = (int32_t*)take(N * 4);
-  S.episode = (int32_t*)take(N * 4);
-  S.scan_valid = (int32_t*)take(N * 4);
+  S.freal = (R*)take(F_NREAL * stride * sizeof(R));
+  S.fint = (int32_t*)take(I_NINT * stride * 4);
+  S.fstride = (int)stride;
   S.obst = (R4<R>*)take(N * cap * sizeof(R4<R>));
   S.sensor_last = (R*)take(N * kSensors * sizeof(R));
   S.asmc = (R*)take((size_t)kAsmcN * N * sizeof(R));
-  R* co = (R*)take(kSensors * sizeof(R));
-  R* so = (R*)take(kSensors * sizeof(R));
-  S.ray_co = co;
-  S.ray_so = so;
+  R* tab = (R*)take(2 * kSensors * sizeof(R));
+  S.ray_tab = tab;
   S.N = h->cfg.num_envs;
   S.cap = h->cfg.obstacle_cap;
   S.limit = h->cfg.max_episode_steps;
@@ -778,19 +850,18 @@ int carve(Handle* h, State<R>& S) {
   S.seed = h->cfg.seed;
   S.gid0 = h->cfg.env_id_offset;
   // ray offsets start + i*res (usv_asmc_ca_env.py:420), cos/sin in float64 on the host
-  std::vector<R> hc(kSensors), hs(kSensors);
+  std::vector<R> ht(2 * kSensors);
   const double span = (2.0 / 3.0) * (2.0 * kPi), res = span / kSensors;
   for (int i = 0; i < kSensors; ++i) {
     const double a = -kPi * 2.0 / 3.0 + i * res;
-    hc[i] = (R)std::cos(a);
-    hs[i] = (R)std::sin(a);
+    ht[i] = (R)std::cos(a);
+    ht[kSensors + i] = (R)std::sin(a);
   }
-  HIP_TRY(hipMemcpy(co, hc.data(), kSensors * sizeof(R), hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(so, hs.data(), kSensors * sizeof(R), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(tab, ht.data(), 2 * kSensors * sizeof(R), hipMemcpyHostToDevice));
   // reference __init__ defaults: max_action = [3, 0, 3] (simple_env.py:32)
   std::vector<R> three(N, (R)3);
-  HIP_TRY(hipMemcpy(S.f[F_MAX_U], three.data(), N * sizeof(R), hipMemcpyHostToDevice));
-  HIP_TRY(hipMemcpy(S.f[F_MAX_R], three.data(), N * sizeof(R), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(S.F(F_MAX_U), three.data(), N * sizeof(R), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(S.F(F_MAX_R), three.data(), N * sizeof(R), hipMemcpyHostToDevice));
   return USV_OK;
 }
 
@@ -799,6 +870,16 @@ int carve(Handle* h, State<R>& S) {
 
 template <typename R, int MODE, int EPB>
 void* pick_lid(int lid) {
+  if constexpr (std::is_same<R, float>::value && MODE == USV_MODE_SIMPLE) {
+    switch (lid) {
+      case 0: return (void*)&step_kernel_tight<R, MODE, EPB, 0>;
+      case 1: return (void*)&step_kernel_tight<R, MODE, EPB, 1>;
+      case 2: return (void*)&step_kernel_tight<R, MODE, EPB, 2>;
+      case 3: return (void*)&step_kernel_tight<R, MODE, EPB, 3>;
+      case 5: return (void*)&step_kernel_tight<R, MODE, EPB, 5>;
+      default: return (void*)&step_kernel_tight<R, MODE, EPB, 7>;
+    }
+  }
   switch (lid) {
     case 0: return (void*)&step_kernel<R, MODE, EPB, 0>;
     case 1: return (void*)&step_kernel<R, MODE, EPB, 1>;
@@ -833,9 +914,9 @@ int launch_reset(Handle* h, State<R>& S, const uint8_t* mask, float* obs, hipStr
   IO<R> io{nullptr, obs, nullptr, nullptr, nullptr, nullptr, mask};
   const dim3 grid((S.N + kEPBReset - 1) / kEPBReset), block(kBlock);
   if (h->cfg.mode == USV_MODE_SIMPLE)
-    hipLaunchKernelGGL((reset_kernel<R, USV_MODE_SIMPLE>), grid, block, lds_bytes<R>(0, S.cap), st, S, io);
+    hipLaunchKernelGGL((reset_kernel<R, USV_MODE_SIMPLE>), grid, block, lds_head_bytes<R>() + kWaves * 3 * 64 * sizeof(R), st, S, io);
   else
-    hipLaunchKernelGGL((reset_kernel<R, USV_MODE_ASMC_SIMPLE>), grid, block, lds_bytes<R>(0, S.cap), st, S, io);
+    hipLaunchKernelGGL((reset_kernel<R, USV_MODE_ASMC_SIMPLE>), grid, block, lds_head_bytes<R>() + kWaves * 3 * 64 * sizeof(R), st, S, io);
   HIP_TRY(hipGetLastError());
   return USV_OK;
 }
@@ -856,17 +937,16 @@ int field_io(Handle* h, State<R>& S, int f, void* host, bool to_host) {
     std::vector<R> tmp(N);
     double* hd = (double*)host;
     if (to_host) {
-      HIP_TRY(hipMemcpy(tmp.data(), S.f[f], N * sizeof(R), hipMemcpyDeviceToHost));
+      HIP_TRY(hipMemcpy(tmp.data(), S.F(f), N * sizeof(R), hipMemcpyDeviceToHost));
       for (size_t i = 0; i < N; ++i) hd[i] = (double)tmp[i];
     } else {
       for (size_t i = 0; i < N; ++i) tmp[i] = (R)hd[i];
-      HIP_TRY(hipMemcpy(S.f[f], tmp.data(), N * sizeof(R), hipMemcpyHostToDevice));
+      HIP_TRY(hipMemcpy(S.F(f), tmp.data(), N * sizeof(R), hipMemcpyHostToDevice));
     }
     return USV_OK;
   }
   if (f >= USV_FIELD_N_OBS && f <= USV_FIELD_SCAN_VALID) {
-    int32_t* d = f == USV_FIELD_N_OBS ? S.n_obs : f == USV_FIELD_ELAPSED ? S.elapsed
-               : f == USV_FIELD_EPISODE ? S.episode : S.scan_valid;
+    int32_t* d = S.I(f - USV_FIELD_N_OBS);
     if (!to_host && f == USV_FIELD_N_OBS) {
       const int32_t* hv = (const int32_t*)host;
       for (size_t i = 0; i < N; ++i)
@@ -1023,7 +1103,7 @@ int usv_seed(void* hp, uint64_t seed) {
   h->cfg.seed = seed;
   h->sf.seed = seed;
   h->sd.seed = seed;
-  int32_t* ep = h->cfg.precision == USV_F32 ? h->sf.episode : h->sd.episode;
+  int32_t* ep = h->cfg.precision == USV_F32 ? h->sf.I(I_EPISODE) : h->sd.I(I_EPISODE);
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemset(ep, 0, (size_t)h->cfg.num_envs * 4));
   return USV_OK;
