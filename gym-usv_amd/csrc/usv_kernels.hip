@@ -442,7 +442,7 @@ __device__ __forceinline__ void lidar_brute(R dx, R dy, R r2, R key, R d, R rr, 
 // instead of 128 x n.
 struct WinLds {
   unsigned long long* slot;   // [128] per wave, ~0 between envs
-  int* mark;                  // [64]  per wave
+  volatile int* mark;         // [64]  per wave (cross-lane through LDS: volatile + wave fence)
   const float2* rayoff;       // [128] block-shared ray offset table
   const float* lx;            // this env's obstacle row (LDS SoA)
   const float* ly;
@@ -492,6 +492,8 @@ __device__ __forceinline__ void lidar_window(float dx, float dy, float key, floa
     // owner of pair q = base + l: the obstacle whose run of pairs starts at or before q
     L.mark[l] = -1;
     if (cnt > 0 && off >= base && off < base + kWave) L.mark[off - base] = l;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");   // other lanes' marks must be read
+    __builtin_amdgcn_wave_barrier();
     const int j = max(wave_incl_max(L.mark[l]), carry);
     carry = __builtin_amdgcn_readlane(j, 63);
     const int q = base + l;
@@ -511,6 +513,8 @@ __device__ __forceinline__ void lidar_window(float dx, float dy, float key, floa
     if ((q < W) & (proj >= 0.0f) & (delta >= 0.0f))
       atomicMin(&L.slot[i], ((unsigned long long)gk << 32) | (unsigned)jj);
   }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");     // all lanes' ds_min_u64 landed
+  __builtin_amdgcn_wave_barrier();
   const unsigned long long v0 = L.slot[l], v1 = L.slot[l + 64];
   L.slot[l] = ~0ull;                                  // re-arm for this wave's next env
   L.slot[l + 64] = ~0ull;
@@ -540,7 +544,7 @@ template <typename R> struct EnvLds {
 template <typename R, int LID>
 __device__ __forceinline__ void lidar_wave(const EnvLds<R>& E, int n, R px, R py, R sp, R cp,
                                            const typename Vec2<R>::T* rayoff, unsigned long long* slot,
-                                           int* mark, Scan<R>& out) {
+                                           volatile int* mark, Scan<R>& out) {
   const int l = lane_id();
   const bool valid = l < n;
   const R ox = valid ? E.lx[l] : R(0), oy = valid ? E.ly[l] : R(0), rr = valid ? E.lr[l] : R(0);
