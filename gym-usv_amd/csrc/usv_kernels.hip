@@ -442,7 +442,7 @@ __device__ __forceinline__ void lidar_brute(R dx, R dy, R r2, R key, R d, R rr, 
 // instead of 128 x n.
 struct WinLds {
   unsigned long long* slot;   // [128] per wave, ~0 between envs
-  volatile int* mark;         // [64]  per wave (cross-lane through LDS: volatile + wave fence)
+  int* mark;                  // [64]  per wave (cross-lane through LDS: ordered by a wave fence)
   const float2* rayoff;       // [128] block-shared ray offset table
   const float* lx;            // this env's obstacle row (LDS SoA)
   const float* ly;
@@ -544,7 +544,7 @@ template <typename R> struct EnvLds {
 template <typename R, int LID>
 __device__ __forceinline__ void lidar_wave(const EnvLds<R>& E, int n, R px, R py, R sp, R cp,
                                            const typename Vec2<R>::T* rayoff, unsigned long long* slot,
-                                           volatile int* mark, Scan<R>& out) {
+                                           int* mark, Scan<R>& out) {
   const int l = lane_id();
   const bool valid = l < n;
   const R ox = valid ? E.lx[l] : R(0), oy = valid ? E.ly[l] : R(0), rr = valid ? E.lr[l] : R(0);

@@ -435,3 +435,202 @@ class OracleVectorEnv:
             obs = obs.copy()
             obs[idx] = self.env.obs(np.zeros((self.env.n, 3)))[idx]
         return obs, rew, term, trunc, final_obs, done
+
+
+# --------------------------------------------------------------------------- usv-asmc-v0 (legacy)
+# UsvAsmcEnv coefficients that differ from UsvAsmc (usv_asmc_env.py:20,51-53,74-78)
+V0_MIN_SPEED = 0.3
+V0_K_AK, V0_K_YE, V0_SIGMA_YE = 5.72, 0.5, 1.0
+V0_MAX_ACTION = np.pi / 2
+V0_C_ACTION = 1.0 / np.power((V0_MAX_ACTION / 2 - (-V0_MAX_ACTION) / 2) / H, 2)   # :77
+V0_W_ACTION = 0.2                                                                 # :78
+V0_T_MIN, V0_T_MAX = -30.0, 36.5                                                  # :182-185
+f32 = np.float32
+
+
+class AsmcV0Batch:
+    """Batched restatement of the legacy ``UsvAsmcEnv`` (id usv-asmc-v0, usv_asmc_env.py:14-401).
+
+    One 0.01 s ASMC + Gonzalez-Garcia plant step per env step with a sigmoid desired speed
+    (:151-156), no r_d filter (e_psi_dot = -r, :149), thrust saturation (:182-185) and the
+    float32 rounding the reference applies: T, CRB, CA, Dl, Dn, J are float32 arrays
+    (:191-222) and the whole state is stored as float32 after every step (:247-251).  Scalars
+    follow NumPy 2 promotion (a float32 operand with Python scalars stays float32).  Quirk:
+    e_u_last is never updated (:159, :251).  obs = [u, v_ak, r, ye, psi_ak, action_last].
+    Resets draw from a per-env ``np.random.RandomState`` exactly like the reference's global
+    ``np.random.uniform`` calls (:260-279) after ``np.random.seed(seed)``.
+    """
+
+    obs_dim = 6
+    act_dim = 1
+
+    def __init__(self, n):
+        self.n = n
+        z = lambda *s: np.zeros((n,) + s)
+        self.velocity, self.position, self.aux = z(3), z(3), z(3)
+        self.last = z(9)
+        self.target = z(6)          # x_0, y_0, desired_speed, ak, x_d, y_d
+        self.state = z(6)
+        self.first = np.ones(n, bool)   # reference state is float64 until the first step
+        self.rngs = [None] * n
+
+    def reset_env(self, i, seed=None):
+        if seed is not None or self.rngs[i] is None:
+            self.rngs[i] = np.random.RandomState(seed)
+        g = self.rngs[i]
+        x, y = g.uniform(-2.5, 2.5), g.uniform(-2.5, 2.5)                  # :260-261
+        psi = g.uniform(-np.pi, np.pi)                                     # :262
+        x0, y0 = g.uniform(-2.5, 2.5), g.uniform(-2.5, 2.5)                # :275-276
+        xd = g.uniform(15, 30)                                             # :277
+        yd = y0                                                            # :278
+        ds = g.uniform(1.4, 2.4)                                           # :279
+        ak = float(f32(math.atan2(yd - y0, xd - x0)))                      # :281-282
+        psi_ak = float(f32(wrap_once(np.float64(psi - ak))))              # :284-286
+        ye = -(x - x0) * math.sin(ak) + (y - y0) * math.cos(ak)            # :287
+        self.velocity[i] = 0.0
+        self.position[i] = [x, y, psi]
+        self.aux[i] = 0.0
+        self.last[i] = 0.0
+        self.target[i] = [x0, y0, ds, ak, xd, yd]
+        # body_to_path(0, 0, psi_ak) -> v_ak = 0 (:289)
+        self.state[i] = [0.0, 0.0, 0.0, ye, psi_ak, 0.0]
+        self.first[i] = True
+
+    def reset(self, seeds=None, idx=None):
+        idx = range(self.n) if idx is None else idx
+        for k, i in enumerate(idx):
+            self.reset_env(i, None if seeds is None else seeds[k])
+        return self.state.astype(np.float32)
+
+    def step(self, action):
+        """action [N] (or [N,1]) heading offsets; returns obs [N,6] f32, reward [N], done [N]."""
+        a = np.asarray(action, dtype=np.float32).reshape(self.n)
+        fs = ~self.first                         # envs whose stored state is float32
+        u, v, r = (self.velocity[:, k] for k in range(3))
+        x, y, psi = (self.position[:, k] for k in range(3))
+        e_u_int, ka_u, ka_psi = (self.aux[:, k] for k in range(3))
+        xd_l, yd_l, pd_l, ud_l, vd_l, rd_l, e_u_last, kdu_l, kdp_l = (self.last[:, k] for k in range(9))
+        x0, y0, ds, ak = (self.target[:, k] for k in range(4))
+        a_last = self.state[:, 5]
+        # action_dot: float32 once the stored state is float32 (:120)
+        ad64 = (a.astype(np.float64) - a_last) / H
+        ad32 = ((a - a_last.astype(np.float32)) / np.float32(H)).astype(np.float64)
+        action_dot = np.where(fs, ad32, ad64)
+        psi_d = wrap_once(a.astype(np.float64) + ak)                      # :123-124
+        fast = np.abs(u) > 1.2                                             # :126-130
+
+        def f32ops(vals):
+            """Evaluate in float32 where the env's state is float32 (NumPy 2 promotion)."""
+            return np.where(fs, vals(np.float32).astype(np.float64), vals(np.float64))
+
+        def hydro(dt):
+            uu, vv, rr = u.astype(dt), v.astype(dt), r.astype(dt)
+            mag = np.sqrt(np.power(uu, 2) + np.power(vv, 2))
+            yv = dt(0.5) * (dt(-40 * 1000) * np.abs(vv)) * dt(1.1 + 0.0045 * (1.01 / 0.09) - 0.1 * (0.27 / 0.09) + 0.016 * np.power((0.27 / 0.09), 2))
+            yr = dt(6 * (-3.141592 * 1000)) * mag * dt(0.09) * dt(0.09) * dt(1.01)
+            nv = dt(0.06 * (-3.141592 * 1000)) * mag * dt(0.09) * dt(0.09) * dt(1.01)
+            nr = dt(0.02 * (-3.141592 * 1000)) * mag * dt(0.09) * dt(0.09) * dt(1.01) * dt(1.01)
+            return yv, yr, nv, nr
+        y64, y32 = hydro(np.float64), hydro(np.float32)
+        yv, yr, nv, nr = (np.where(fs, b.astype(np.float64), c) for b, c in zip(y32, y64))   # :132-139
+        xu = np.where(fast, 64.55, -25.0)
+        xuu = np.where(fast, -70.92, 0.0)
+
+        def fpart(dt):
+            uu, vv, rr = u.astype(dt), v.astype(dt), r.astype(dt)
+            fu = (dt(MASS - Y_V_DOT) * vv * rr + (xuu.astype(dt) * np.abs(uu) + xu.astype(dt) * uu)) / dt(MASS - X_U_DOT)
+            fp = (dt(-X_U_DOT + Y_V_DOT) * uu * vv + (nr.astype(dt) * rr)) / dt(IZ - N_R_DOT)
+            return fu, fp
+        fu32, fp32 = fpart(np.float32)
+        fu64, fp64 = fpart(np.float64)
+        f_u = np.where(fs, fu32.astype(np.float64), fu64)                  # :144
+        f_psi = np.where(fs, fp32.astype(np.float64), fp64)                # :145
+        e_psi = wrap_once(psi_d - psi)                                     # :147-148
+        e_psi_dot = 0 - r                                                  # :149
+        u_psi = 1 / (1 + np.exp(10 * (np.abs(e_psi) * (2 / np.pi) - 0.5)))    # :153
+        u_d = (ds - V0_MIN_SPEED) * u_psi + V0_MIN_SPEED                   # :155-156
+        e_u = u_d - u                                                      # :158
+        e_u_int = H * (e_u + e_u_last) / 2 + e_u_int                       # :159 (e_u_last stale)
+        sig_u = e_u + LAMBDA_U * e_u_int                                   # :161
+        sig_p = e_psi_dot + LAMBDA_PSI * e_psi                             # :162
+        kdu = np.where(ka_u > KMIN_U, K_U * np.sign(np.abs(sig_u) - MU_U), KMIN_U)       # :164
+        kdp = np.where(ka_psi > KMIN_PSI, K_PSI * np.sign(np.abs(sig_p) - MU_PSI), KMIN_PSI)
+        ka_u = H * (kdu + kdu_l) / 2 + ka_u                                # :167
+        ka_psi = H * (kdp + kdp_l) / 2 + ka_psi                            # :170
+        ua_u = -ka_u * np.sqrt(np.abs(sig_u)) * np.sign(sig_u) - K2_U * sig_u            # :173
+        ua_p = -ka_psi * np.sqrt(np.abs(sig_p)) * np.sign(sig_p) - K2_PSI * sig_p        # :174
+        tx = (LAMBDA_U * e_u - f_u - ua_u) / (1 / (MASS - X_U_DOT))       # :176
+        tz = (LAMBDA_PSI * e_psi - f_psi - ua_p) / (1 / (IZ - N_R_DOT))   # :177
+        tport = np.clip(tx / 2 + tz / B_TH, V0_T_MIN, V0_T_MAX)            # :179-185
+        tstbd = np.clip(tx / (2 * C_TH) - tz / (B_TH * C_TH), V0_T_MIN, V0_T_MAX)
+        t0 = (tport + C_TH * tstbd).astype(np.float32)                     # :191 float32 T
+        t2 = (0.5 * B_TH * (tport - C_TH * tstbd)).astype(np.float32)
+        # CRB, CA, Dl, Dn as float32 arrays (:193-212), entries computed in the stored dtype
+        uu, vv, rr = u.astype(np.float32), v.astype(np.float32), r.astype(np.float32)
+
+        def cast(z):
+            return z.astype(np.float32)
+        m = np.float32(MASS)
+        c02 = cast(np.where(fs, (0 - m * vv).astype(np.float64), 0 - MASS * v)) + cast(np.where(fs, (np.float32(2) * (np.float32(Y_V_DOT) * vv + np.float32((Y_R_DOT + N_V_DOT) / 2) * rr)).astype(np.float64), 2 * (Y_V_DOT * v + ((Y_R_DOT + N_V_DOT) / 2) * r)))
+        c12 = cast(np.where(fs, (m * uu).astype(np.float64), MASS * u)) + cast(np.where(fs, (0 - np.float32(X_U_DOT * MASS) * uu).astype(np.float64), 0 - X_U_DOT * MASS * u))
+        c20 = cast(np.where(fs, (m * vv).astype(np.float64), MASS * v)) + cast(np.where(fs, (np.float32(2) * ((np.float32(-Y_V_DOT) * vv) - np.float32((Y_R_DOT + N_V_DOT) / 2) * rr)).astype(np.float64), 2 * ((-Y_V_DOT) * v - ((Y_R_DOT + N_V_DOT) / 2) * r)))
+        c21 = cast(np.where(fs, (0 - m * uu).astype(np.float64), 0 - MASS * u)) + cast(np.where(fs, (np.float32(X_U_DOT * MASS) * uu).astype(np.float64), X_U_DOT * MASS * u))
+        av = np.where(fs, np.abs(vv).astype(np.float64), np.abs(v))
+        ar = np.where(fs, np.abs(rr).astype(np.float64), np.abs(r))
+        d00 = cast(0 - xu) - cast(xuu * np.abs(u))
+        d11 = cast(0 - yv) - cast(f32ops(lambda dt: dt(YVV) * av.astype(dt) + dt(YVR) * ar.astype(dt)))
+        d12 = cast(0 - yr) - cast(f32ops(lambda dt: dt(YRV) * av.astype(dt) + dt(YRR) * ar.astype(dt)))
+        d21 = cast(0 - nv) - cast(f32ops(lambda dt: dt(NVV) * av.astype(dt) + dt(NVR) * ar.astype(dt)))
+        d22 = cast(0 - nr) - cast(f32ops(lambda dt: dt(NRV) * av.astype(dt) + dt(NRR) * ar.astype(dt)))
+        # T - C nu - D nu: float32 products/sums where nu is float32, float64 on the first step
+        def rhs(dt):
+            U, V, Rr = u.astype(dt), v.astype(dt), r.astype(dt)
+            cn0 = c02.astype(dt) * Rr
+            cn1 = c12.astype(dt) * Rr
+            cn2 = c20.astype(dt) * U + c21.astype(dt) * V
+            dn0 = d00.astype(dt) * U
+            dn1 = d11.astype(dt) * V + d12.astype(dt) * Rr
+            dn2 = d21.astype(dt) * V + d22.astype(dt) * Rr
+            return ((t0.astype(dt) - cn0) - dn0, (dt(0) - cn1) - dn1, (t2.astype(dt) - cn2) - dn2)
+        r32, r64 = rhs(np.float32), rhs(np.float64)
+        rhs0, rhs1, rhs2 = (np.where(fs, b.astype(np.float64), c) for b, c in zip(r32, r64))
+        ud = M_INV[0, 0] * rhs0 + M_INV[0, 1] * rhs1 + M_INV[0, 2] * rhs2               # :214-215
+        vd = M_INV[1, 0] * rhs0 + M_INV[1, 1] * rhs1 + M_INV[1, 2] * rhs2
+        rd = M_INV[2, 0] * rhs0 + M_INV[2, 1] * rhs1 + M_INV[2, 2] * rhs2
+        u = H * (ud + ud_l) / 2 + u                                        # :216-217
+        v = H * (vd + vd_l) / 2 + v
+        r = H * (rd + rd_l) / 2 + r
+        # J is a float32 array (:220-222): cos/sin of the stored (float32) heading, or of the
+        # float64 reset heading on the first step, rounded to float32
+        psif = psi.astype(np.float32)
+        cj = np.where(fs, np.cos(psif).astype(np.float64), np.cos(psi).astype(np.float32).astype(np.float64))
+        sj = np.where(fs, np.sin(psif).astype(np.float64), np.sin(psi).astype(np.float32).astype(np.float64))
+        xd = cj * u - sj * v                                               # :224
+        yd = sj * u + cj * v
+        pd = r
+        x = H * (xd + xd_l) / 2 + x                                        # :225
+        y = H * (yd + yd_l) / 2 + y
+        psi = H * (pd + pd_l) / 2 + psi
+        psi = wrap_once(psi)                                               # :228-229
+        psi_ak = wrap_once(psi - ak)                                       # :231-232
+        ye = -(x - x0) * np.sin(ak) + (y - y0) * np.cos(ak)                # :234
+        ye_abs = np.abs(ye)
+        # compute_reward (:364-374)
+        pa = np.abs(psi_ak)
+        ad = np.where(fs, np.power(action_dot.astype(np.float32), 2).astype(np.float64), np.power(action_dot, 2))
+        cad = np.where(fs, (np.float32(-V0_C_ACTION) * ad.astype(np.float32)).astype(np.float64), -V0_C_ACTION * ad)
+        r_act = V0_W_ACTION * np.tanh(cad)
+        r_ye = np.where(ye_abs > V0_SIGMA_YE, np.exp(-V0_K_YE * ye_abs), np.exp(-V0_K_YE * np.power(ye_abs, 2) / V0_SIGMA_YE))
+        r_ak = -np.exp(V0_K_AK * (pa - np.pi))
+        reward = np.where(pa < np.pi / 2, r_act + r_ye, r_ak)
+        v_ak = np.sin(psi_ak) * u + np.cos(psi_ak) * v                     # body_to_path :376-390
+        done = (ye_abs > 10) | (np.abs(x) > 30)                             # :241-245
+        reward = np.where(done, -1.0, reward)
+        q = lambda z: z.astype(np.float32).astype(np.float64)              # stored float32 (:247-251)
+        self.state = np.stack([q(u), q(v_ak), q(r), q(ye), q(psi_ak), a.astype(np.float64)], axis=1)
+        self.velocity = np.stack([q(u), q(v), q(r)], axis=1)
+        self.position = np.stack([q(x), q(y), q(psi)], axis=1)
+        self.aux = np.stack([q(e_u_int), q(ka_u), q(ka_psi)], axis=1)
+        self.last = np.stack([q(xd), q(yd), q(pd), q(ud), q(vd), q(rd), q(e_u_last), q(kdu), q(kdp)], axis=1)
+        self.first[:] = False
+        return self.state.astype(np.float32), reward, done

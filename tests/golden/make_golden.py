@@ -13,6 +13,7 @@ reference source travels.  Fixtures:
 * ``simple_traj.npz``    -- UsvSimpleEnv (usv-simple) seeded reset + random-action rollouts with
                             TimeLimit + same-step autoreset (SB3 DummyVecEnv semantics).
 * ``asmc_simple_traj.npz`` -- the same for UsvSimpleASMCEnv (usv-asmc-simple).
+* ``asmc_v0_traj.npz``   -- legacy UsvAsmcEnv (usv-asmc-v0) seeded rollouts with resets on done.
 """
 from __future__ import annotations
 
@@ -150,6 +151,41 @@ def gen_traj(E, cls, fname, limit, n_env=8, T=96):
     print(fname, "episodes ended:", int((term | trunc).sum()), "terminated:", int(term.sum()))
 
 
+def gen_asmc_v0(E, fname="asmc_v0_traj.npz", n_env=4, T=3000):
+    """Legacy UsvAsmcEnv (usv-asmc-v0, usv_asmc_env.py:99-300): old gym API, scalar action,
+    np.random global RNG for resets (seeded per env here), no TimeLimit.  On done the env is
+    reset (continuing the global stream), like a DummyVecEnv would."""
+    rng = np.random.default_rng(11)
+    acts = rng.uniform(-np.pi / 2, np.pi / 2, size=(n_env, T))
+    # envs 1.. steer off the path (heading offsets biased away) so episodes end (|ye| > 10)
+    for e in range(1, n_env):
+        acts[e] = np.clip(rng.normal((-1) ** e * (0.6 + 0.3 * e), 0.3, size=T), -np.pi / 2, np.pi / 2)
+    acts = acts.astype(np.float32)
+    seeds = np.arange(n_env) + 2000
+    obs0 = np.zeros((n_env, 6), np.float32)
+    obs = np.zeros((n_env, T, 6), np.float32)
+    fobs = np.zeros((n_env, T, 6), np.float32)
+    rew = np.zeros((n_env, T))
+    done = np.zeros((n_env, T), bool)
+    init = {k: [] for k in ("state", "velocity", "position", "aux_vars", "last", "target")}
+    for e in range(n_env):
+        np.random.seed(int(seeds[e]))
+        env = E.UsvAsmcEnv()
+        obs0[e] = env.reset()
+        for k in init:
+            init[k].append(np.array(getattr(env, k), dtype=np.float64))
+        for t in range(T):
+            o, r, d, _ = env.step(acts[e, t])      # scalar action (shape-(1,) raises on NumPy >= 1.24)
+            fobs[e, t], rew[e, t], done[e, t] = o, r, bool(d)
+            if d:
+                o = env.reset()
+            obs[e, t] = o
+    np.savez_compressed(os.path.join(HERE, fname), seeds=seeds, actions=acts, obs0=obs0, obs=obs,
+                        final_obs=fobs, reward=rew, done=done,
+                        **{f"init_{k}": np.stack(v) for k, v in init.items()})
+    print(fname, "episodes ended:", int(done.sum()))
+
+
 def main():
     refharness.load_reference()
     import gym_usv.envs as E
@@ -159,6 +195,7 @@ def main():
     gen_traj(E, E.UsvSimpleASMCEnv, "asmc_simple_traj.npz", 1000, n_env=6, T=160)
     # short time limit variant exercises TimeLimit truncation + autoreset path
     gen_traj(E, E.UsvSimpleEnv, "simple_traj_tl.npz", 20, n_env=4, T=64)
+    gen_asmc_v0(E)
 
 
 if __name__ == "__main__":

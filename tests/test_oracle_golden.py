@@ -78,3 +78,25 @@ def test_trajectories_match_reference(golden, fname, env_id):
         np.testing.assert_allclose(rew, g["reward"][:, t], rtol=1e-9, atol=1e-9, err_msg=f"t={t}")
         np.testing.assert_allclose(fobs, g["final_obs"][:, t], rtol=1e-6, atol=1e-6, err_msg=f"t={t}")
         np.testing.assert_allclose(obs, g["obs"][:, t], rtol=1e-6, atol=1e-6, err_msg=f"t={t}")
+
+
+def test_asmc_v0_trajectories_match_reference(golden):
+    """Legacy usv-asmc-v0 (usv_asmc_env.py:99-300): seeded resets (np.random), 3000 scalar-action
+    steps per env with resets on done; float32 state rounding reproduced."""
+    g = golden("asmc_v0_traj.npz")
+    n, T = g["actions"].shape
+    o = O.AsmcV0Batch(n)
+    obs = o.reset([int(s) for s in g["seeds"]])
+    np.testing.assert_array_equal(obs, g["obs0"])
+    np.testing.assert_allclose(o.position, g["init_position"], atol=0)
+    np.testing.assert_allclose(o.target, g["init_target"], atol=0)
+    for t in range(T):
+        ob, rw, dn = o.step(g["actions"][:, t])
+        np.testing.assert_array_equal(dn, g["done"][:, t], err_msg=f"t={t}")
+        np.testing.assert_allclose(ob, g["final_obs"][:, t], rtol=0, atol=5e-6, err_msg=f"t={t}")
+        np.testing.assert_allclose(rw, g["reward"][:, t], rtol=0, atol=1e-6, err_msg=f"t={t}")
+        if dn.any():
+            idx = np.flatnonzero(dn)
+            o.reset(idx=idx)
+            np.testing.assert_array_equal(o.state[idx].astype(np.float32), g["obs"][idx, t])
+    assert g["done"].sum() >= 5
