@@ -48,13 +48,16 @@ template <typename R> struct State {
   R4<R>* obst;             // [N][cap] (x, y, r, r*r)
   R* sensor_last;          // [N][128]
   R* asmc;                 // [16][N]
+  R* v0;                   // [19][fstride] usv-asmc-v0: last[9], aux[3], target[6], action_last
   const R* ray_tab;        // [2][128] cos / sin(start + i*res)
   int N, cap, limit, autoreset;
   int fstride;             // elements between fields (>= N, 256-B aligned)
   uint64_t seed, gid0;
   __host__ __device__ R* F(int i) const { return freal + (size_t)i * fstride; }
   __host__ __device__ int32_t* I(int i) const { return fint + (size_t)i * fstride; }
+  __host__ __device__ R* V(int i) const { return v0 + (size_t)i * fstride; }
 };
+constexpr int kV0Last = 0, kV0Aux = 9, kV0Target = 12, kV0ALast = 18, kV0N = 19;
 
 template <typename R> struct IO {
   const float* act;        // [N][2]
@@ -778,6 +781,169 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(State<R> S, IO<R> io) {
   }
 }
 
+// --------------------------------------------------------------------------- usv-asmc-v0
+// Legacy UsvAsmcEnv (id usv-asmc-v0, usv_asmc_env.py:14-401): one 0.01 s ASMC + plant step per
+// env step, lane-per-env, no lidar.  The reference stores its state as float32 after every
+// step (:247-251) and builds T, CRB, CA, Dl, Dn, J as float32 arrays (:191-222); NumPy 2 keeps
+// scalar arithmetic on float32 operands in float32.  Those rounding points are reproduced
+// (q32 / float arithmetic) so the f64 build tracks the reference to float32 rounding; the
+// first step after a reset runs on the float64 reset state (:258-300), flagged by elapsed == 0.
+constexpr double kV0MinSpeed = 0.3, kV0KAk = 5.72, kV0KYe = 0.5, kV0SigmaYe = 1.0;
+constexpr double kV0CAction = 1.0 / (((kPi / 2) / 2 - (-kPi / 2) / 2) / H * (((kPi / 2) / 2 - (-kPi / 2) / 2) / H));
+constexpr double kV0WAction = 0.2, kV0TMin = -30.0, kV0TMax = 36.5;
+
+template <typename R> __device__ __forceinline__ R q32(R x) { return R((float)x); }
+
+template <typename R>
+__device__ __forceinline__ void v0_obs(float* row, R u, R v_ak, R r, R ye, R psi_ak, R a_last) {
+  row[0] = (float)u; row[1] = (float)v_ak; row[2] = (float)r;
+  row[3] = (float)ye; row[4] = (float)psi_ak; row[5] = (float)a_last;
+}
+
+// UsvAsmcEnv.reset (usv_asmc_env.py:258-300); Philox draws replace np.random.uniform
+template <typename R>
+__device__ void v0_reset(const State<R>& S, int e, float* row) {
+  const int ep = S.I(I_EPISODE)[e];
+  Philox g(S.seed, S.gid0 + (uint64_t)e, (uint32_t)ep);
+  const double x = g.uniform(-2.5, 2.5), y = g.uniform(-2.5, 2.5);               // :260-261
+  const double psi = g.uniform(-kPi, kPi);                                        // :262
+  const double x0 = g.uniform(-2.5, 2.5), y0 = g.uniform(-2.5, 2.5);             // :275-276
+  const double xd = g.uniform(15.0, 30.0), yd = y0;                              // :277-278
+  const double ds = g.uniform(1.4, 2.4);                                          // :279
+  const double ak = (double)(float)atan2(yd - y0, xd - x0);                       // :281-282
+  const double psi_ak = (double)(float)wrap_once(psi - ak);                       // :284-286
+  const double ye = -(x - x0) * sin(ak) + (y - y0) * cos(ak);                     // :287
+  S.F(F_X)[e] = R(x); S.F(F_Y)[e] = R(y); S.F(F_PSI)[e] = R(psi);
+  S.F(F_U)[e] = R(0); S.F(F_V)[e] = R(0); S.F(F_R)[e] = R(0);
+  for (int i = 0; i < kV0Target; ++i) S.V(i)[e] = R(0);                          // last, aux
+  const double tg[6] = {x0, y0, ds, ak, xd, yd};
+  for (int i = 0; i < 6; ++i) S.V(kV0Target + i)[e] = R(tg[i]);
+  S.V(kV0ALast)[e] = R(0);
+  S.I(I_ELAPSED)[e] = 0;
+  S.I(I_EPISODE)[e] = ep + 1;
+  v0_obs<R>(row, R(0), R(0), R(0), R(ye), R(psi_ak), R(0));                      // :289-298
+}
+
+template <typename R>
+__global__ __launch_bounds__(kBlock) void v0_step_kernel(State<R> S, IO<R> io) {
+  const int e = blockIdx.x * kBlock + threadIdx.x;
+  if (e >= S.N) return;
+  const bool first = S.I(I_ELAPSED)[e] == 0;        // reference state still float64 (reset arrays)
+  const float af = io.act[e];
+  const R a = R(af);
+  R u = S.F(F_U)[e], v = S.F(F_V)[e], r = S.F(F_R)[e];
+  R x = S.F(F_X)[e], y = S.F(F_Y)[e], psi = S.F(F_PSI)[e];
+  R e_u_int = S.V(kV0Aux)[e], ka_u = S.V(kV0Aux + 1)[e], ka_psi = S.V(kV0Aux + 2)[e];
+  const R xd_l = S.V(0)[e], yd_l = S.V(1)[e], pd_l = S.V(2)[e];
+  const R ud_l = S.V(3)[e], vd_l = S.V(4)[e], rd_l = S.V(5)[e];
+  const R e_u_last = S.V(6)[e], kdu_l = S.V(7)[e], kdp_l = S.V(8)[e];
+  const R x0 = S.V(kV0Target)[e], y0 = S.V(kV0Target + 1)[e], ds = S.V(kV0Target + 2)[e];
+  const R ak = S.V(kV0Target + 3)[e];
+  const R a_last = S.V(kV0ALast)[e];
+  // action_dot (:120): float32 arithmetic once the stored state is float32
+  const R action_dot = first ? (a - a_last) / R(H) : R((af - (float)a_last) / (float)H);
+  const R psi_d = wrap_once(a + ak);                                             // :123-124
+  const bool fast = m_abs(u) > R(1.2);                                           // :126-130
+  const R xu = fast ? R(64.55) : R(-25.0), xuu = fast ? R(-70.92) : R(0.0);
+  // hydrodynamic terms, f, C, D: float32 (state is float32; exactly 0 on the first step)
+  const float uf = (float)u, vf = (float)v, rf = (float)r;
+  const float mag = sqrtf(uf * uf + vf * vf);
+  const float yv = (0.5f * (-40000.0f * fabsf(vf))) *
+                   (float)(1.1 + 0.0045 * (1.01 / 0.09) - 0.1 * (0.27 / 0.09) + 0.016 * ((0.27 / 0.09) * (0.27 / 0.09)));  // :132
+  const float yr = (((float)(6 * (-3.141592 * 1000)) * mag) * 0.09f) * 0.09f * 1.01f;            // :134
+  const float nv = (((float)(0.06 * (-3.141592 * 1000)) * mag) * 0.09f) * 0.09f * 1.01f;         // :136
+  const float nr = (((float)(0.02 * (-3.141592 * 1000)) * mag) * 0.09f) * 0.09f * 1.01f * 1.01f; // :138
+  const float fu = ((float)(MASS - Y_V_DOT) * vf * rf + ((float)xuu * fabsf(uf) + (float)xu * uf)) / (float)(MASS - X_U_DOT);  // :144
+  const float fpsi = ((float)(-X_U_DOT + Y_V_DOT) * uf * vf + (nr * rf)) / (float)(IZ - N_R_DOT);                             // :145
+  const R e_psi = wrap_once(psi_d - psi);                                        // :147-148
+  const R e_psi_dot = R(0) - r;                                                  // :149
+  const R u_psi = R(1) / (R(1) + m_exp(R(10) * (m_abs(e_psi) * R(2 / kPi) - R(0.5))));  // :153
+  const R u_d = (ds - R(kV0MinSpeed)) * u_psi + R(kV0MinSpeed);                  // :155-156
+  const R e_u = u_d - u;                                                         // :158
+  e_u_int = R(H) * (e_u + e_u_last) / R(2) + e_u_int;                            // :159 (e_u_last stale)
+  const R sig_u = e_u + R(LAMBDA_U) * e_u_int;                                   // :161
+  const R sig_p = e_psi_dot + R(LAMBDA_PSI) * e_psi;                             // :162
+  const R kdu = ka_u > R(KMIN_U) ? R(K_U) * m_sign(m_abs(sig_u) - R(MU_U)) : R(KMIN_U);       // :164
+  const R kdp = ka_psi > R(KMIN_PSI) ? R(K_PSI) * m_sign(m_abs(sig_p) - R(MU_PSI)) : R(KMIN_PSI);
+  ka_u = R(H) * (kdu + kdu_l) / R(2) + ka_u;                                     // :167
+  ka_psi = R(H) * (kdp + kdp_l) / R(2) + ka_psi;                                 // :170
+  const R ua_u = -ka_u * m_sqrt(m_abs(sig_u)) * m_sign(sig_u) - R(K2_U) * sig_u;           // :173
+  const R ua_p = -ka_psi * m_sqrt(m_abs(sig_p)) * m_sign(sig_p) - R(K2_PSI) * sig_p;       // :174
+  const R tx = (R(LAMBDA_U) * e_u - R(fu) - ua_u) / R(1.0 / (MASS - X_U_DOT));  // :176
+  const R tz = (R(LAMBDA_PSI) * e_psi - R(fpsi) - ua_p) / R(1.0 / (IZ - N_R_DOT));
+  const R tport = m_clip(tx / R(2) + tz / R(B_TH), R(kV0TMin), R(kV0TMax));      // :179-185
+  const R tstbd = m_clip(tx / R(2 * C_TH) - tz / R(B_TH * C_TH), R(kV0TMin), R(kV0TMax));
+  const float t0 = (float)(tport + R(C_TH) * tstbd);                             // :191 float32 T
+  const float t2 = (float)(R(0.5 * B_TH) * (tport - R(C_TH) * tstbd));
+  // C = CRB + CA, D = Dl - Dn as float32 (:193-212)
+  const float c02 = (0.0f - 30.0f * vf) + 2.0f * ((float)Y_V_DOT * vf + (float)((Y_R_DOT + N_V_DOT) / 2) * rf);
+  const float c12 = (30.0f * uf) + (0.0f - (float)(X_U_DOT * MASS) * uf);
+  const float c20 = (30.0f * vf) + 2.0f * (((float)(0 - Y_V_DOT) * vf) - (float)((Y_R_DOT + N_V_DOT) / 2) * rf);
+  const float c21 = (0.0f - 30.0f * uf) + ((float)(X_U_DOT * MASS) * uf);
+  const float av = fabsf(vf), ar = fabsf(rf);
+  const float d00 = (float)(0 - xu) - (float)(xuu * m_abs(u));
+  const float d11 = (0.0f - yv) - ((float)YVV * av + (float)YVR * ar);
+  const float d12 = (0.0f - yr) - ((float)YRV * av + (float)YRR * ar);
+  const float d21 = (0.0f - nv) - ((float)NVV * av + (float)NVR * ar);
+  const float d22 = (0.0f - nr) - ((float)NRV * av + (float)NRR * ar);
+  // T - C nu - D nu (:214-215), float32 (nu is float32 after the first step, 0 on it)
+  const float rhs0 = (t0 - c02 * rf) - d00 * uf;
+  const float rhs1 = (0.0f - c12 * rf) - (d11 * vf + d12 * rf);
+  const float rhs2 = (t2 - (c20 * uf + c21 * vf)) - (d21 * vf + d22 * rf);
+  const R ud = R(MI00) * R(rhs0);                                                // :214 M^-1 (f64)
+  const R vd = R(MI11) * R(rhs1) + R(MI12) * R(rhs2);
+  const R rd = R(MI21) * R(rhs1) + R(MI22) * R(rhs2);
+  u = R(H) * (ud + ud_l) / R(2) + u;                                             // :216-217
+  v = R(H) * (vd + vd_l) / R(2) + v;
+  r = R(H) * (rd + rd_l) / R(2) + r;
+  // J as float32 (:220-222): of the float32 heading, or the float64 reset heading rounded
+  const R cj = first ? R((float)m_cos(psi)) : R(cosf((float)psi));
+  const R sj = first ? R((float)m_sin(psi)) : R(sinf((float)psi));
+  const R xd = cj * u - sj * v, yd = sj * u + cj * v, pd = r;                    // :224
+  x = R(H) * (xd + xd_l) / R(2) + x;                                             // :225
+  y = R(H) * (yd + yd_l) / R(2) + y;
+  psi = wrap_once(R(H) * (pd + pd_l) / R(2) + psi);                              // :228-229
+  const R psi_ak = wrap_once(psi - ak);                                          // :231-232
+  const R ye = -(x - x0) * m_sin(ak) + (y - y0) * m_cos(ak);                     // :234
+  const R ye_abs = m_abs(ye);
+  // compute_reward (:364-374)
+  const R pa = m_abs(psi_ak);
+  const R cad = first ? R(-kV0CAction) * (action_dot * action_dot)
+                      : R((float)(-kV0CAction) * ((float)action_dot * (float)action_dot));
+  const R r_act = R(kV0WAction) * tanh(cad);
+  const R r_ye = ye_abs > R(kV0SigmaYe) ? m_exp(R(-kV0KYe) * ye_abs) : m_exp(R(-kV0KYe) * (ye_abs * ye_abs) / R(kV0SigmaYe));
+  const R r_ak = -m_exp(R(kV0KAk) * (pa - R(kPi)));
+  const R v_ak = m_sin(psi_ak) * u + m_cos(psi_ak) * v;                          // body_to_path :376-390
+  const bool done = ye_abs > R(10) || m_abs(x) > R(30);                          // :241-245
+  const int el = S.I(I_ELAPSED)[e] + 1;
+  const bool trunc = !done && S.limit > 0 && el >= S.limit;
+  io.rew[e] = done ? R(-1) : (pa < R(kPi / 2) ? r_act + r_ye : r_ak);
+  io.term[e] = done;
+  io.trunc[e] = trunc;
+  float* row = io.obs + (size_t)e * 6;
+  // stored state (float32, :247-251)
+  S.F(F_U)[e] = q32(u); S.F(F_V)[e] = q32(v); S.F(F_R)[e] = q32(r);
+  S.F(F_X)[e] = q32(x); S.F(F_Y)[e] = q32(y); S.F(F_PSI)[e] = q32(psi);
+  S.V(kV0Aux)[e] = q32(e_u_int); S.V(kV0Aux + 1)[e] = q32(ka_u); S.V(kV0Aux + 2)[e] = q32(ka_psi);
+  S.V(0)[e] = q32(xd); S.V(1)[e] = q32(yd); S.V(2)[e] = q32(pd);
+  S.V(3)[e] = q32(ud); S.V(4)[e] = q32(vd); S.V(5)[e] = q32(rd);
+  S.V(6)[e] = q32(e_u_last); S.V(7)[e] = q32(kdu); S.V(8)[e] = q32(kdp);
+  S.V(kV0ALast)[e] = a;
+  S.I(I_ELAPSED)[e] = el;
+  v0_obs<R>(row, u, v_ak, r, ye, psi_ak, a);
+  if (done || trunc) {
+    if (io.fobs) v0_obs<R>(io.fobs + (size_t)e * 6, u, v_ak, r, ye, psi_ak, a);
+    if (S.autoreset == USV_AUTORESET_SAME_STEP) v0_reset<R>(S, e, row);
+  }
+}
+
+template <typename R>
+__global__ __launch_bounds__(kBlock) void v0_reset_kernel(State<R> S, IO<R> io) {
+  const int e = blockIdx.x * kBlock + threadIdx.x;
+  if (e >= S.N || (io.mask && !io.mask[e])) return;
+  v0_reset<R>(S, e, io.obs + (size_t)e * 6);
+}
+
 }  // namespace usv
 
 // ============================================================================= host side
@@ -804,7 +970,8 @@ const FieldDesc kFields[USV_FIELD_COUNT] = {
     {"x", 0}, {"y", 0}, {"psi", 0}, {"u", 0}, {"v", 0}, {"r", 0}, {"last_u", 0}, {"last_r", 0},
     {"progress", 0}, {"path_x0", 0}, {"path_y0", 0}, {"path_x1", 0}, {"path_y1", 0},
     {"max_u", 0}, {"max_r", 0}, {"ref_v", 0}, {"n_obs", 1}, {"elapsed", 1}, {"episode", 1},
-    {"scan_valid", 1}, {"obs_x", 0}, {"obs_y", 0}, {"obs_r", 0}, {"sensor_last", 0}, {"asmc", 0}};
+    {"scan_valid", 1}, {"obs_x", 0}, {"obs_y", 0}, {"obs_r", 0}, {"sensor_last", 0}, {"asmc", 0},
+    {"v0_last", 0}, {"v0_aux", 0}, {"v0_target", 0}, {"v0_action_last", 0}};
 
 struct Handle {
   usv_config cfg;
@@ -834,7 +1001,8 @@ int carve(Handle* h, State<R>& S) {
   const size_t stride = al(N * sizeof(R)) / sizeof(R);   // also >= N int32 (sizeof(R) >= 4)
   const size_t bytes = F_NREAL * stride * sizeof(R) + al(I_NINT * stride * 4) +
                        al(N * cap * sizeof(R4<R>)) + al(N * kSensors * sizeof(R)) +
-                       al((size_t)kAsmcN * N * sizeof(R)) + al(2 * kSensors * sizeof(R));
+                       al((size_t)kAsmcN * N * sizeof(R)) + al((size_t)kV0N * stride * sizeof(R)) +
+                       al(2 * kSensors * sizeof(R));
   HIP_TRY(hipMalloc(&h->slab, bytes));
   HIP_TRY(hipMemset(h->slab, 0, bytes));
   char* p = (char*)h->slab;
@@ -845,6 +1013,7 @@ int carve(Handle* h, State<R>& S) {
   S.obst = (R4<R>*)take(N * cap * sizeof(R4<R>));
   S.sensor_last = (R*)take(N * kSensors * sizeof(R));
   S.asmc = (R*)take((size_t)kAsmcN * N * sizeof(R));
+  S.v0 = (R*)take((size_t)kV0N * stride * sizeof(R));
   R* tab = (R*)take(2 * kSensors * sizeof(R));
   S.ray_tab = tab;
   S.N = h->cfg.num_envs;
@@ -904,6 +1073,11 @@ template <typename R>
 int launch_step(Handle* h, State<R>& S, const float* act, float* obs, void* rew, uint8_t* term,
                 uint8_t* trunc, float* fobs, hipStream_t st) {
   IO<R> io{act, obs, (R*)rew, term, trunc, fobs, nullptr};
+  if (h->cfg.mode == USV_MODE_ASMC_V0) {
+    hipLaunchKernelGGL((v0_step_kernel<R>), dim3((S.N + kBlock - 1) / kBlock), dim3(kBlock), 0, st, S, io);
+    HIP_TRY(hipGetLastError());
+    return USV_OK;
+  }
   const int epb = h->epb, lid = h->lid;
   void* fn = h->cfg.mode == USV_MODE_SIMPLE ? pick_step<R, USV_MODE_SIMPLE>(epb, lid)
                                             : pick_step<R, USV_MODE_ASMC_SIMPLE>(epb, lid);
@@ -917,7 +1091,9 @@ template <typename R>
 int launch_reset(Handle* h, State<R>& S, const uint8_t* mask, float* obs, hipStream_t st) {
   IO<R> io{nullptr, obs, nullptr, nullptr, nullptr, nullptr, mask};
   const dim3 grid((S.N + kEPBReset - 1) / kEPBReset), block(kBlock);
-  if (h->cfg.mode == USV_MODE_SIMPLE)
+  if (h->cfg.mode == USV_MODE_ASMC_V0)
+    hipLaunchKernelGGL((v0_reset_kernel<R>), dim3((S.N + kBlock - 1) / kBlock), dim3(kBlock), 0, st, S, io);
+  else if (h->cfg.mode == USV_MODE_SIMPLE)
     hipLaunchKernelGGL((reset_kernel<R, USV_MODE_SIMPLE>), grid, block, lds_head_bytes<R>() + kWaves * 3 * 64 * sizeof(R), st, S, io);
   else
     hipLaunchKernelGGL((reset_kernel<R, USV_MODE_ASMC_SIMPLE>), grid, block, lds_head_bytes<R>() + kWaves * 3 * 64 * sizeof(R), st, S, io);
@@ -929,7 +1105,16 @@ int field_per_env(const Handle* h, int f) {
   if (f >= USV_FIELD_OBS_X && f <= USV_FIELD_OBS_R) return h->cfg.obstacle_cap;
   if (f == USV_FIELD_SENSOR_LAST) return kSensors;
   if (f == USV_FIELD_ASMC) return kAsmcN;
+  if (f == USV_FIELD_V0_LAST) return 9;
+  if (f == USV_FIELD_V0_AUX) return 3;
+  if (f == USV_FIELD_V0_TARGET) return 6;
   return 1;
+}
+
+// first v0 SoA row of a v0 field
+int v0_base(int f) {
+  return f == USV_FIELD_V0_LAST ? kV0Last : f == USV_FIELD_V0_AUX ? kV0Aux
+       : f == USV_FIELD_V0_TARGET ? kV0Target : kV0ALast;
 }
 
 // host <-> device for one field; host side [N][per] float64 / int32
@@ -1004,6 +1189,21 @@ int field_io(Handle* h, State<R>& S, int f, void* host, bool to_host) {
     }
     return USV_OK;
   }
+  if (f >= USV_FIELD_V0_LAST && f <= USV_FIELD_V0_ACTION_LAST) {   // device SoA rows, host [N][per]
+    const int per = field_per_env(h, f), base = v0_base(f);
+    std::vector<R> tmp(N);
+    double* hd = (double*)host;
+    for (int i = 0; i < per; ++i) {
+      if (to_host) {
+        HIP_TRY(hipMemcpy(tmp.data(), S.V(base + i), N * sizeof(R), hipMemcpyDeviceToHost));
+        for (size_t e = 0; e < N; ++e) hd[e * per + i] = (double)tmp[e];
+      } else {
+        for (size_t e = 0; e < N; ++e) tmp[e] = (R)hd[e * per + i];
+        HIP_TRY(hipMemcpy(S.V(base + i), tmp.data(), N * sizeof(R), hipMemcpyHostToDevice));
+      }
+    }
+    return USV_OK;
+  }
   return fail(USV_ERR_ARG, "unknown field");
 }
 
@@ -1037,7 +1237,7 @@ void usv_config_default(usv_config* cfg, int32_t mode, int32_t num_envs) {
   cfg->precision = USV_F32;
   cfg->num_envs = num_envs;
   cfg->obstacle_cap = 32;
-  cfg->max_episode_steps = mode == USV_MODE_ASMC_SIMPLE ? 1000 : 500;   // gym_usv/__init__.py:27,33
+  cfg->max_episode_steps = mode == USV_MODE_ASMC_SIMPLE ? 1000 : mode == USV_MODE_ASMC_V0 ? 0 : 500;  // gym_usv/__init__.py
   cfg->autoreset = USV_AUTORESET_SAME_STEP;
   cfg->lidar_algo = USV_LIDAR_WINDOW;
   cfg->seed = 0;
@@ -1048,7 +1248,7 @@ int usv_create(const usv_config* cfg, int32_t device, void** out) {
   if (!cfg || !out) return fail(USV_ERR_ARG, "null argument");
   *out = nullptr;
   if (cfg->abi_version != USV_ABI_VERSION) return fail(USV_ERR_ABI, "abi_version mismatch");
-  if (cfg->mode != USV_MODE_SIMPLE && cfg->mode != USV_MODE_ASMC_SIMPLE)
+  if (cfg->mode != USV_MODE_SIMPLE && cfg->mode != USV_MODE_ASMC_SIMPLE && cfg->mode != USV_MODE_ASMC_V0)
     return fail(USV_ERR_ARG, "unknown mode");
   if (cfg->precision != USV_F32 && cfg->precision != USV_F64)
     return fail(USV_ERR_ARG, "unknown precision");
@@ -1095,7 +1295,12 @@ void usv_destroy(void* hp) {
 }
 
 int usv_num_envs(void* hp) { return hp ? as_handle(hp)->cfg.num_envs : fail(USV_ERR_ARG, "null handle"); }
-int usv_obs_dim(void* hp) { return hp ? kObsDim : fail(USV_ERR_ARG, "null handle"); }
+int usv_obs_dim(void* hp) {
+  return hp ? (as_handle(hp)->cfg.mode == USV_MODE_ASMC_V0 ? 6 : kObsDim) : fail(USV_ERR_ARG, "null handle");
+}
+int usv_act_dim(void* hp) {
+  return hp ? (as_handle(hp)->cfg.mode == USV_MODE_ASMC_V0 ? 1 : 2) : fail(USV_ERR_ARG, "null handle");
+}
 int usv_reward_bytes(void* hp) {
   return hp ? (as_handle(hp)->cfg.precision == USV_F64 ? 8 : 4) : fail(USV_ERR_ARG, "null handle");
 }

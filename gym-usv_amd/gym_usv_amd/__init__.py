@@ -4,6 +4,7 @@ Registry mirroring gym_usv/__init__.py:3-39 for the ids on the accelerated path:
 
     make("usv-simple")                         -> UsvSimpleEnv with TimeLimit(500)
     make("usv-asmc-simple")                    -> UsvSimpleASMCEnv with TimeLimit(1000)
+    make("usv-asmc-v0")                        -> legacy UsvAsmcEnv (old gym API, no TimeLimit)
     make_vec("usv-simple", num_envs=65536)     -> UsvVectorEnv (one HIP launch per step)
 
 The compute lives in libusvhip.so (HIP, gfx950) behind the C-ABI in include/usv_hip.h.
@@ -13,14 +14,16 @@ from .vector_env import ENV_SPECS, UsvVectorEnv  # noqa: F401
 
 __all__ = ["make", "make_vec", "registry", "UsvVectorEnv", "UsvLibError", "ENV_SPECS"]
 
-registry = {k: {"entry_point": f"gym_usv_amd.envs:{cls}", "max_episode_steps": v[1]}
-            for (k, v), cls in zip(ENV_SPECS.items(), ("UsvSimpleEnv", "UsvSimpleASMCEnv"))}
+registry = {k: {"entry_point": f"gym_usv_amd.envs:{cls}", "max_episode_steps": v[1] or None}
+            for (k, v), cls in zip(ENV_SPECS.items(), ("UsvSimpleEnv", "UsvSimpleASMCEnv", "UsvAsmcEnv"))}
 
 
 def make(env_id, max_episode_steps=None, **kwargs):
     from . import envs
-    cls = {"usv-simple": envs.UsvSimpleEnv, "usv-asmc-simple": envs.UsvSimpleASMCEnv}[env_id]
+    cls = {"usv-simple": envs.UsvSimpleEnv, "usv-asmc-simple": envs.UsvSimpleASMCEnv,
+           "usv-asmc-v0": envs.UsvAsmcEnv}[env_id]
     limit = registry[env_id]["max_episode_steps"] if max_episode_steps is None else max_episode_steps
+    limit = limit or 0
     return cls(max_episode_steps=limit, **kwargs)
 
 

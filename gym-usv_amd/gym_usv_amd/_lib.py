@@ -15,7 +15,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 LIB_PATH = os.environ.get("USV_LIB_PATH", LIB_PATH)
 
 ABI_VERSION = 1
-MODE_SIMPLE, MODE_ASMC_SIMPLE = 0, 1
+MODE_SIMPLE, MODE_ASMC_SIMPLE, MODE_ASMC_V0 = 0, 1, 2
 F32, F64 = 0, 1
 AUTORESET_SAME_STEP, AUTORESET_DISABLED = 0, 1
 LIDAR_BRUTE, LIDAR_WINDOW = 0, 1
@@ -44,6 +44,7 @@ SIGNATURES = [
     ("usv_destroy", None, [_vp]),
     ("usv_num_envs", ctypes.c_int, [_vp]),
     ("usv_obs_dim", ctypes.c_int, [_vp]),
+    ("usv_act_dim", ctypes.c_int, [_vp]),
     ("usv_reward_bytes", ctypes.c_int, [_vp]),
     ("usv_seed", ctypes.c_int, [_vp, _u64]),
     ("usv_reset", ctypes.c_int, [_vp, _vp, _vp, _vp]),

@@ -41,7 +41,8 @@ class _SingleEnv:
         return obs[0].cpu().numpy(), {}
 
     def step(self, action):
-        a = torch.as_tensor(np.asarray(action, dtype=np.float32).reshape(1, 2), device=self._venv.device)
+        a = torch.as_tensor(np.asarray(action, dtype=np.float32).reshape(1, self._venv.act_dim),
+                            device=self._venv.device)
         obs, rew, term, trunc, _ = self._venv.step(a)
         return (obs[0].cpu().numpy(), float(rew[0].item()), bool(term[0].item()),
                 bool(trunc[0].item()), {})
@@ -58,3 +59,17 @@ class UsvSimpleEnv(_SingleEnv):
 class UsvSimpleASMCEnv(_SingleEnv):
     """HIP-backed ``UsvSimpleASMCEnv`` (id usv-asmc-simple)."""
     env_id = "usv-asmc-simple"
+
+
+class UsvAsmcEnv(_SingleEnv):
+    """HIP-backed legacy ``UsvAsmcEnv`` (id usv-asmc-v0, usv_asmc_env.py:14) with the reference's
+    old gym API: ``reset() -> obs`` and ``step(action) -> (obs, reward, done, info)``."""
+    env_id = "usv-asmc-v0"
+
+    def reset(self, seed=None, options=None):
+        obs, _ = super().reset(seed=seed, options=options)
+        return obs
+
+    def step(self, action):
+        obs, r, term, trunc, info = super().step(action)
+        return obs, r, term or trunc, info

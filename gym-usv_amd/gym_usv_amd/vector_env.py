@@ -18,10 +18,22 @@ from . import _lib
 from .spaces import Box
 
 ENV_SPECS = {
-    # id: (mode, max_episode_steps)  -- gym_usv/__init__.py:24-34
+    # id: (mode, max_episode_steps)  -- gym_usv/__init__.py:3-34
     "usv-simple": (_lib.MODE_SIMPLE, 500),
     "usv-asmc-simple": (_lib.MODE_ASMC_SIMPLE, 1000),
+    "usv-asmc-v0": (_lib.MODE_ASMC_V0, 0),      # registered without max_episode_steps (:3-6)
 }
+
+
+def _spaces(env_id):
+    """Observation / action spaces as the reference declares them."""
+    if env_id == "usv-asmc-v0":                  # usv_asmc_env.py:74-96
+        lo = np.array([-1.5, -1.5, -1.0, -10, -np.pi, -np.pi / 2], dtype=np.float32)
+        hi = np.array([1.5, 1.5, 1.0, 10, np.pi, np.pi / 2], dtype=np.float32)
+        return (Box(lo, hi, dtype=np.float32),
+                Box(-np.pi / 2, np.pi / 2, shape=(1,), dtype=np.float32))
+    return (Box(-1, 1, shape=(_lib.OBS_DIM,), dtype=np.float32),          # simple_env.py:27,30
+            Box(np.array([0.2, -1]), np.array([1, 1]), shape=(2,), dtype=np.float32))
 
 
 def _stream_ptr(device):
@@ -71,17 +83,17 @@ class UsvVectorEnv:
             _lib.check(self.lib.usv_create(ctypes.byref(cfg), self.device.index, ctypes.byref(h)))
         self._h = h
         n = self.num_envs
+        self.obs_dim = self.lib.usv_obs_dim(h)
+        self.act_dim = self.lib.usv_act_dim(h)
         rdt = torch.float32 if precision == "f32" else torch.float64
         kw = dict(device=self.device)
-        self.obs = torch.zeros((n, _lib.OBS_DIM), dtype=torch.float32, **kw)
-        self.final_obs = torch.zeros((n, _lib.OBS_DIM), dtype=torch.float32, **kw)
+        self.obs = torch.zeros((n, self.obs_dim), dtype=torch.float32, **kw)
+        self.final_obs = torch.zeros((n, self.obs_dim), dtype=torch.float32, **kw)
         self.reward = torch.zeros(n, dtype=rdt, **kw)
         self._term = torch.zeros(n, dtype=torch.uint8, **kw)
         self._trunc = torch.zeros(n, dtype=torch.uint8, **kw)
         self.max_episode_steps = cfg.max_episode_steps
-        # spaces (simple_env.py:27,30)
-        self.single_observation_space = Box(-1, 1, shape=(_lib.OBS_DIM,), dtype=np.float32)
-        self.single_action_space = Box(np.array([0.2, -1]), np.array([1, 1]), shape=(2,), dtype=np.float32)
+        self.single_observation_space, self.single_action_space = _spaces(env_id)
         self._fields = self._field_table()
 
     # ------------------------------------------------------------------ API
@@ -100,8 +112,10 @@ class UsvVectorEnv:
         a = torch.as_tensor(actions, device=self.device)
         if a.dtype != torch.float32 or not a.is_contiguous():
             a = a.to(torch.float32).contiguous()
-        if a.shape != (self.num_envs, _lib.ACT_DIM):
-            raise ValueError(f"actions must be [{self.num_envs}, 2], got {tuple(a.shape)}")
+        if self.act_dim == 1 and a.shape == (self.num_envs,):
+            a = a.reshape(self.num_envs, 1)
+        if a.shape != (self.num_envs, self.act_dim):
+            raise ValueError(f"actions must be [{self.num_envs}, {self.act_dim}], got {tuple(a.shape)}")
         _lib.check(self.lib.usv_step(self._h, _ptr(a), _ptr(self.obs), _ptr(self.reward),
                                      _ptr(self._term), _ptr(self._trunc), _ptr(self.final_obs),
                                      _stream_ptr(self.device)))

@@ -337,3 +337,97 @@ def test_step_variants_bit_identical(env_id, precision, monkeypatch):
         for t, (a_, b_) in enumerate(zip(ref, outs)):
             for x, y in zip(a_, b_):
                 assert torch.equal(x, y), f"variant {v} differs at step {t}"
+
+
+# --------------------------------------------------------------------------- usv-asmc-v0 (legacy)
+def _v0_inject(env, o, first):
+    env.set_state({"x": o.position[:, 0], "y": o.position[:, 1], "psi": o.position[:, 2],
+                   "u": o.velocity[:, 0], "v": o.velocity[:, 1], "r": o.velocity[:, 2],
+                   "v0_last": o.last, "v0_aux": o.aux, "v0_target": o.target,
+                   "v0_action_last": o.state[:, 5], "elapsed": np.where(first, 0, 1)})
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_v0_golden_trajectory_replay(golden, precision):
+    """Reference usv-asmc-v0 rollouts (usv_asmc_env.py:99-255) replayed from the reference's reset
+    state, autoreset off, up to each env's first done."""
+    g = golden("asmc_v0_traj.npz")
+    n, T = g["actions"].shape
+    env = make("usv-asmc-v0", n, precision=precision, autoreset=False)
+    o = O.AsmcV0Batch(n)
+    o.reset([int(s) for s in g["seeds"]])
+    _v0_inject(env, o, np.ones(n, bool))
+    alive = np.ones(n, bool)
+    worst_o = worst_r = 0.0
+    tol_o, tol_r = (5e-6, 1e-6) if precision == "f64" else (2e-3, 2e-3)
+    steps = T if precision == "f64" else 600      # f32 state drifts along chaotic ASMC switches
+    for t in range(steps):
+        obs, rew, term, trunc, _ = env.step(torch.from_numpy(g["actions"][:, t:t + 1]).cuda())
+        obs, rew, term = to_np(obs, rew, term)
+        m = alive
+        if not m.any():
+            break
+        worst_o = max(worst_o, float(np.abs(obs[m] - g["final_obs"][m, t]).max()))
+        worst_r = max(worst_r, float(np.abs(rew[m] - g["reward"][m, t]).max()))
+        np.testing.assert_array_equal(term[m], g["done"][m, t], err_msg=f"t={t}")
+        alive = alive & ~g["done"][:, t]
+    print(f"\n[golden asmc_v0 {precision}] max |obs| err {worst_o:.3e}, max |rew| err {worst_r:.3e}")
+    assert worst_o <= tol_o and worst_r <= tol_r
+    env.close()
+
+
+@pytest.mark.parametrize("precision", ["f32", "f64"])
+def test_v0_single_step_parity_4096(precision):
+    n = 4096
+    o = O.AsmcV0Batch(n)
+    o.reset(list(range(n)))
+    rng = np.random.default_rng(3)
+    first = np.ones(n, bool)
+    for _ in range(40):
+        _, _, dn = o.step(rng.uniform(-np.pi / 2, np.pi / 2, n).astype(np.float32))
+        first[:] = False
+        if dn.any():
+            o.reset(idx=np.flatnonzero(dn))
+            first[dn] = True
+    env = make("usv-asmc-v0", n, precision=precision, autoreset=True)
+    for k in range(3):
+        _v0_inject(env, o, first)
+        a = rng.uniform(-np.pi / 2, np.pi / 2, n).astype(np.float32)
+        obs, rew, term, trunc, info = env.step(torch.from_numpy(a).cuda())
+        g_obs, g_rew, g_term, g_fobs = to_np(obs, rew, term, info["final_obs"])
+        o_obs, o_rew, o_done = o.step(a)
+        first[:] = False
+        assert (g_term != o_done).sum() <= 1
+        ok = g_term == o_done
+        rows = np.where((g_term & ok)[:, None], g_fobs, g_obs)
+        tol = 2e-6 if precision == "f64" else 2e-4
+        err = np.abs(rows[ok] - o_obs[ok])
+        print(f"[v0 {precision} round {k}] obs max err {err.max():.3e}, reward max err "
+              f"{np.abs(g_rew[ok] - o_rew[ok]).max():.3e}, done {int(o_done.sum())}")
+        assert err.max() <= tol
+        assert np.abs(g_rew[ok] - o_rew[ok]).max() <= (1e-6 if precision == "f64" else 1e-3)
+        if o_done.any():
+            idx = np.flatnonzero(o_done)
+            o.reset(idx=idx)
+            first[idx] = True
+    env.close()
+
+
+def test_v0_reset_distribution():
+    from scipy import stats
+    n = 8192
+    env = make("usv-asmc-v0", n, seed=5)
+    obs, _ = env.reset(seed=5)
+    (obs,) = to_np(obs)
+    g = env.get_state()
+    o = O.AsmcV0Batch(n)
+    o_obs = o.reset(list(range(n)))
+    tg = g["v0_target"]
+    for name, a, b in (("x", g["x"], o.position[:, 0]), ("psi", g["psi"], o.position[:, 2]),
+                       ("x0", tg[:, 0], o.target[:, 0]), ("speed", tg[:, 2], o.target[:, 2]),
+                       ("x_d", tg[:, 4], o.target[:, 4]), ("ye", obs[:, 3], o_obs[:, 3])):
+        p = stats.ks_2samp(a, b).pvalue
+        print(f"KS v0 {name}: p={p:.3g}")
+        assert p > 1e-4, name
+    assert np.all(tg[:, 3] == 0) and np.all(obs[:, [0, 1, 2, 5]] == 0)     # ak == 0 (y_d = y_0)
+    env.close()
