@@ -21,6 +21,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import multiprocessing as mp
 import os
 import sys
@@ -40,6 +41,10 @@ def algorithmic_bytes_per_env_step(env_id, mean_obs, precision="f32"):
     """Bytes one env-step must move (DESIGN.md 'Algorithmic bytes'): action in, obs/reward/flags
     out, dynamic state read+write, obstacle read (x, y, r per obstacle).  Reset traffic excluded."""
     w = 4 if precision == "f32" else 8
+    if env_id == "usv-asmc-v0":
+        # action 4, obs 6 f32, reward, flags; state read: pose+velocity (6) + last/aux/target/
+        # action_last (19) + elapsed; write: 6 + 13 (target is read-only) + elapsed
+        return 4 + 6 * 4 + w + 2 + (25 * w + 4) + (19 * w + 4)
     act, obs, rew, flags = 8, 143 * 4, w, 2
     state_rd = 16 * w + 2 * 4          # 16 real fields + n_obs + elapsed
     state_wr = 9 * w + 2 * 4           # pose, velocity, last action, progress + elapsed, scan flag
@@ -77,12 +82,24 @@ def _cpu_worker(args):
     os.environ.setdefault("OMP_NUM_THREADS", "1")
     import numpy as np
     from oracle import usv_oracle as O
-    venv = O.OracleVectorEnv(env_id, 1)
-    venv.reset([seed])
     rng = np.random.default_rng(seed)
+    if env_id == "usv-asmc-v0":
+        o = O.AsmcV0Batch(1)
+        o.reset([seed])
+
+        def one():
+            _, _, d = o.step(rng.uniform(-np.pi / 2, np.pi / 2, 1).astype(np.float32))
+            if d[0]:
+                o.reset(idx=[0])
+    else:
+        venv = O.OracleVectorEnv(env_id, 1)
+        venv.reset([seed])
+
+        def one():
+            venv.step(rng.uniform([0.2, -1], [1, 1], size=(1, 2)).astype(np.float32))
     n, t0 = 0, time.perf_counter()
     while True:
-        venv.step(rng.uniform([0.2, -1], [1, 1], size=(1, 2)).astype(np.float32))
+        one()
         n += 1
         if n % 32 == 0 and time.perf_counter() - t0 >= seconds:
             break
@@ -108,7 +125,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10000)
     ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
-    ap.add_argument("--env-id", default="usv-simple", choices=["usv-simple", "usv-asmc-simple"])
+    ap.add_argument("--env-id", default="usv-simple", choices=["usv-simple", "usv-asmc-simple", "usv-asmc-v0"])
     ap.add_argument("--precision", default="f32", choices=["f32", "f64"])
     ap.add_argument("--lidar", default="window", choices=["brute", "window"])
     ap.add_argument("--seed", type=int, default=0)
@@ -137,15 +154,18 @@ def main():
                                lidar=args.lidar, env_id_offset=shard(rank, N)[0])
     env.reset(seed=args.seed)
     mean_obs = float(env.get_field("n_obs").mean())
+    A, D = env.act_dim, env.obs_dim
 
     # actions for every timed step resident in HBM before timing (cycled pool if huge)
-    pool = max(1, min(K, (8 << 30) // (N * 8)))
+    pool = max(1, min(K, (8 << 30) // (N * 4 * A)))
     gen = torch.Generator(device=dev).manual_seed(args.seed * 7919 + rank)
-    lo = torch.tensor([0.2, -1.0], device=dev)
-    span = torch.tensor([0.8, 2.0], device=dev)
-    acts = torch.rand((pool, N, 2), device=dev, generator=gen) * span + lo
-    obs = torch.empty((N, 143), device=dev)
-    fobs = torch.empty((N, 143), device=dev)
+    if A == 2:
+        lo, span = torch.tensor([0.2, -1.0], device=dev), torch.tensor([0.8, 2.0], device=dev)
+    else:                                       # usv-asmc-v0 heading offset (usv_asmc_env.py:74-75)
+        lo, span = torch.tensor([-math.pi / 2], device=dev), torch.tensor([math.pi], device=dev)
+    acts = torch.rand((pool, N, A), device=dev, generator=gen) * span + lo
+    obs = torch.empty((N, D), device=dev)
+    fobs = torch.empty((N, D), device=dev)
     rew = torch.empty(N, device=dev, dtype=torch.float32 if args.precision == "f32" else torch.float64)
     term = torch.empty(N, device=dev, dtype=torch.uint8)
     trunc = torch.empty(N, device=dev, dtype=torch.uint8)
@@ -211,6 +231,9 @@ def main():
                          "traffic": traffic, "kernel_ms": round(kern_ms, 5),
                          "algorithmic_bytes_per_env_step": round(bpe, 1)},
         }
+        if args.env_id == "usv-asmc-v0":
+            out["config"].pop("lidar")
+            out["config"].pop("mean_obstacles")
         if not args.no_cpu_baseline:
             procs = args.cpu_procs or min(16, len(os.sched_getaffinity(0)))
             out["cpu_baseline"] = cpu_baseline(args.env_id, args.cpu_seconds, procs)
