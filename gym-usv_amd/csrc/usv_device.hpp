@@ -77,6 +77,13 @@ __device__ __forceinline__ double m_fma(double a, double b, double c) { return f
 __device__ __forceinline__ float  m_abs(float x)  { return fabsf(x); }
 __device__ __forceinline__ double m_abs(double x) { return fabs(x); }
 
+// Fast paths for the f32 build's per-env scalar math (hardware v_sin/v_cos/v_exp, ~1 ulp at
+// the argument ranges here); the f64 build keeps the correctly rounded libm calls.
+__device__ __forceinline__ void fx_sincos(float x, float* s, float* c) { *s = __sinf(x); *c = __cosf(x); }
+__device__ __forceinline__ void fx_sincos(double x, double* s, double* c) { sincos(x, s, c); }
+__device__ __forceinline__ float  fx_exp(float x)  { return __expf(x); }
+__device__ __forceinline__ double fx_exp(double x) { return exp(x); }
+
 template <typename T> __device__ __forceinline__ T m_clip(T x, T lo, T hi) {
   // np.clip(x, lo, hi) == minimum(maximum(x, lo), hi)
   x = x > lo ? x : lo;

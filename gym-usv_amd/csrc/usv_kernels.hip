@@ -218,6 +218,10 @@ __device__ __forceinline__ void reset_wave(const State<R>& S, int e, float* row)
   }
 }
 
+// sin/cos of the heading used by the lidar; the step kernel and the reset kernel (stale scan)
+// must use this same function so their scans are bit-identical
+template <typename R> __device__ __forceinline__ void heading_sincos(R psi, R* s, R* c) { fx_sincos(psi, s, c); }
+
 // --------------------------------------------------------------------------- phase 1
 // UsvSimpleEnv.step kinematics..reward terms (simple_env.py:310-346); for usv-asmc-simple
 // first 2x UsvAsmc.compute (simple_env_asmc.py:18-27) and then step(zeros(2)).
@@ -250,24 +254,26 @@ __device__ void env_dynamics(const State<R>& S, int e, float a_u, float a_r, flo
   v = R(0);
   r = m_clip(r + dvr, -mr, mr);
   R sp, cp;
-  m_sincos(psi, &sp, &cp);
+  fx_sincos(psi, &sp, &cp);
   x = x + (u * cp) * R(kDt);                                                      // :322-324
   y = y + (u * sp) * R(kDt);
   psi = psi + r * R(kDt);
   // _get_closest_point (:139-148)
   const R x0 = S.F(F_PX0)[e], y0 = S.F(F_PY0)[e];
   const R dx = S.F(F_PX1)[e] - x0, dy = S.F(F_PY1)[e] - y0;
-  R a = (dy * (y - y0) + dx * (x - x0)) / (dx * dx + dy * dy);
+  const R det = dx * dx + dy * dy;
+  R a = (dy * (y - y0) + dx * (x - x0)) / det;
   a = a + R(kLookahead);
   a = m_clip(a, S.F(F_PROGRESS)[e], R(1));
   const R tx = x0 + a * dx, ty = y0 + a * dy;
-  // _get_ye (:133-137), _get_angle_to_target (:67-69), distance (:74)
-  const R ak = m_atan2(dy, dx);
-  R sak, cak;
-  m_sincos(ak, &sak, &cak);
+  // _get_ye (:133-137): sin/cos of the path angle a_k = atan2(dy, dx) are dy/|d|, dx/|d|
+  const R inv_len = R(1) / m_sqrt(det);
+  const R sak = dy * inv_len, cak = dx * inv_len;
   const R ye = -(x - x0) * sak + (y - y0) * cak;
+  // _get_angle_to_target (:67-69), distance (:74)
   const R angle = wrap_angle(m_atan2(ty - y, tx - x) - psi);
-  const R dist = m_hypot(x - tx, y - ty);
+  const R ddx = x - tx, ddy = y - ty;
+  const R dist = m_sqrt(ddx * ddx + ddy * ddy);
   const int el = S.I(I_ELAPSED)[e] + 1;
   trunc = (x > R(kBound)) | (x < R(0)) | (y > R(kBound)) | (y < R(0)) |   // :336
           (S.limit > 0 && el >= S.limit);                                 // TimeLimit
@@ -275,10 +281,10 @@ __device__ void env_dynamics(const State<R>& S, int e, float a_u, float a_r, flo
   // _get_reward without the collision term (:150-186)
   const R dact = m_abs(lu - a3u) + m_abs(lr - a3r);
   const R yk = cdiv(ye, kYeK);
-  const R e1 = m_exp(-m_abs(yk)), e2 = m_exp(-(yk * yk));
+  const R e1 = fx_exp(-m_abs(yk)), e2 = fx_exp(-(yk * yk));
   const R ye_r = e1 > e2 ? e1 : e2;
-  const R ang_r = m_exp(-m_abs(angle));
-  const R vel_r = m_exp(-m_abs(m_hypot(u, v) - refv)) * R(0.05);
+  const R ang_r = fx_exp(-m_abs(angle));
+  const R vel_r = fx_exp(-m_abs(m_sqrt(u * u + v * v) - refv)) * R(0.05);
   const R dact_r = -(dact / R(2)) * R(0.15);
   partial = ye_r + ang_r + vel_r + dact_r;
   S.F(F_X)[e] = x; S.F(F_Y)[e] = y; S.F(F_PSI)[e] = psi;
@@ -288,7 +294,7 @@ __device__ void env_dynamics(const State<R>& S, int e, float a_u, float a_r, flo
   S.I(I_ELAPSED)[e] = el;
   S.I(I_SCAN)[e] = 1;
   px = x; py = y;
-  m_sincos(psi, &psp, &pcp);
+  heading_sincos(psi, &psp, &pcp);
 }
 
 // --------------------------------------------------------------------------- lidar
@@ -437,7 +443,7 @@ __device__ __forceinline__ void lidar_brute(R dx, R dy, R r2, R key, R d, R rr, 
 }
 
 // Angular-window lidar (f32).  Lane j computes the ray-index windows its obstacle can touch
-// (conservative: 1.5 rays of margin around an upper bound of asin(r/d), pi/2 when the boat is
+// (conservative: a quarter ray of margin around an upper bound of asin(r/d), pi/2 when the boat is
 // inside it), the (obstacle, ray) pairs are expanded over the lanes (prefix sum; each pair's
 // owner found with LDS start markers and a max-scan), each pair runs the same exact test as
 // the brute loop, and the hit with the smallest (key, index) per ray wins through an LDS
@@ -473,7 +479,9 @@ __device__ __forceinline__ void lidar_window(float dx, float dy, float key, floa
   const float s0r = ray_s(cp, sp, (float)kStartC, (float)kStartS);
   const float a = dx * c0r + dy * s0r, b = dy * c0r - dx * s0r;
   const float phi = fast_atan2(b, a);                 // CCW angle from ray 0; ray i at i*res
-  const float margin = (float)(1.5 * kRes);
+  // |err| of the window edges: fast_atan2 < 2e-5 rad, float rounding ~1e-6 rad; a ray
+  // 1e-5 rad outside the true extent already fails the exact test by ~r*d*1e-5 >> ulp
+  const float margin = (float)(0.25 * kRes);
   const bool inside = d <= rr * 1.001f;
   // asin(x) <= x + (pi/2 - 1) x^3 on [0, 1] (Taylor coefficients >= 0 summing to pi/2 at x = 1)
   const float x = fminf(rr * __builtin_amdgcn_rcpf(d), 1.0f);
@@ -757,7 +765,7 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(State<R> S, IO<R> io) {
     R* last = S.sensor_last + (size_t)e * kSensors;
     if (S.I(I_SCAN)[e]) {
       R sp, cp;
-      m_sincos(S.F(F_PSI)[e], &sp, &cp);
+      heading_sincos(S.F(F_PSI)[e], &sp, &cp);
       const int n = uniform(S.I(I_NOBS)[e]);
       if (l < S.cap) {
         const R4<R> o = S.obst[(size_t)e * S.cap + l];
