@@ -329,7 +329,8 @@ __device__ __forceinline__ void ray_pair(Ray<R>& ra, R jdx, R jdy, R jr2, R jk, 
 
 // Lidar variants (compile-time): bit 0 = drop obstacles wholly inside the rear blind sector
 // before the ray loop, bit 1 = obstacle loop unrolled by two, bit 2 = angular-window pair
-// expansion (f32; falls back to bits 0|1 for f64 and when an obstacle is ~100 m away).
+// expansion (f32 only; f64 uses bits 0|1).  The max-range test of :458 runs only in waves with an
+// obstacle >= 99 m away (wave-uniform template switch).
 constexpr int kLidSkip = 1, kLidUnroll2 = 2, kLidWindow = 4;
 
 template <typename R, bool RANGE_CHECK, bool UNROLL2>
@@ -471,6 +472,7 @@ __device__ __forceinline__ int wave_incl_max(int v) {
   return max(v, l >= 48 ? t2 : l >= 32 ? t1 : l >= 16 ? t0 : -1);
 }
 
+template <bool RANGE_CHECK>
 __device__ __forceinline__ void lidar_window(float dx, float dy, float key, float d, float rr, bool valid,
                                              float px, float py, float sp, float cp, const WinLds& L,
                                              Scan<float>& out) {
@@ -521,7 +523,9 @@ __device__ __forceinline__ void lidar_window(float dx, float dy, float key, floa
     const float proj = fmaf(gdx, c, gdy * s);
     const float perp = fmaf(gdx, s, -(gdy * c));
     const float delta = fmaf(-perp, perp, gr * gr);
-    if ((q < W) & (proj >= 0.0f) & (delta >= 0.0f))
+    bool hit = (q < W) & (proj >= 0.0f) & (delta >= 0.0f);
+    if (RANGE_CHECK) hit = hit && (proj - l_sqrt(delta)) < (float)kSensorMax;   // :458
+    if (hit)
       atomicMin(&L.slot[i], ((unsigned long long)gk << 32) | (unsigned)jj);
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");     // all lanes' ds_min_u64 landed
@@ -565,10 +569,10 @@ __device__ __forceinline__ void lidar_wave(const EnvLds<R>& E, int n, R px, R py
   out.term = __ballot(valid & (key < R(kTermDist))) != 0;                       // :334
   out.far = __ballot(valid & (d >= R(0.99 * kSensorMax))) != 0;
   if constexpr (std::is_same<R, float>::value && (LID & kLidWindow) != 0) {
-    if (!out.far) {
-      lidar_window(dx, dy, key, d, rr, valid, px, py, sp, cp, WinLds{slot, mark, rayoff, E.lx, E.ly, E.lr}, out);
-      return;
-    }
+    const WinLds W{slot, mark, rayoff, E.lx, E.ly, E.lr};
+    if (!out.far) lidar_window<false>(dx, dy, key, d, rr, valid, px, py, sp, cp, W, out);
+    else lidar_window<true>(dx, dy, key, d, rr, valid, px, py, sp, cp, W, out);
+    return;
   }
   const auto t0 = rayoff[l], t1 = rayoff[l + 64];
   lidar_brute<R, LID & (kLidSkip | kLidUnroll2)>(dx, dy, r2, key, d, rr, valid, n, out.far, sp, cp,

@@ -92,7 +92,18 @@ def test_golden_trajectory_replay(golden, fname, env_id, precision):
 
 
 # --------------------------------------------------------------------------- single step @ C2
-def _single_step_round(env_id, n, precision, rounds=4, warm=25, seed=0):
+def _scatter(orc_env, rng):
+    """Spread poses over the whole 100 m field, a quarter of them near the corners, so many envs
+    see obstacles >= 99 m away (the lidar's max-range test, usv_asmc_ca_env.py:458)."""
+    n = orc_env.position.shape[0]
+    xy = rng.uniform(0.3, 99.7, size=(n, 2))
+    k = n // 4
+    xy[:k] = np.clip(rng.choice([1.0, 99.0], size=(k, 2)) + rng.normal(0, 0.5, (k, 2)), 0.05, 99.95)
+    orc_env.position[:, :2] = xy
+    orc_env.position[:, 2] = rng.uniform(-np.pi, np.pi, n)
+
+
+def _single_step_round(env_id, n, precision, rounds=4, warm=25, seed=0, scatter=False):
     orc = O.OracleVectorEnv(env_id, n)
     orc.reset(list(range(seed, seed + n)))
     rng = np.random.default_rng(seed)
@@ -101,6 +112,8 @@ def _single_step_round(env_id, n, precision, rounds=4, warm=25, seed=0):
     env = make(env_id, n, precision=precision, autoreset=True)
     stats = []
     for _ in range(rounds):
+        if scatter:
+            _scatter(orc.env, rng)
         inject(env, orc.env, elapsed=orc.elapsed.astype(np.int32))
         a = rng.uniform([0.2, -1], [1, 1], size=(n, 2)).astype(np.float32)
         obs, rew, term, trunc, info = env.step(torch.from_numpy(a).cuda())
@@ -131,13 +144,16 @@ def _check_rows(g_rows, o_rows, atol, rtol, label):
 
 @pytest.mark.parametrize("env_id", ["usv-simple", "usv-asmc-simple"])
 @pytest.mark.parametrize("precision", ["f32", "f64"])
-def test_single_step_parity_4096(env_id, precision):
+@pytest.mark.parametrize("scatter", [False, True], ids=["near-start", "scattered"])
+def test_single_step_parity_4096(env_id, precision, scatter):
+    """One step from oracle-injected states vs the oracle.  `scattered` spreads the poses over
+    the field so obstacles beyond the 99 m far threshold occur (lidar max-range test)."""
     n = 4096 if env_id == "usv-simple" else 2048
     atol, rtol, ratol = (F32_OBS_ATOL, F32_OBS_RTOL, F32_REW_ATOL) if precision == "f32" else (2e-6, 1e-6, 1e-9)
     if env_id == "usv-asmc-simple" and precision == "f32":
         # 20 ASMC substeps in fp32: r_d = (psi_d - psi_d_last)/0.01 amplifies psi rounding
         atol, rtol, ratol = 5e-4, 1e-3, 5e-3
-    for k, s in enumerate(_single_step_round(env_id, n, precision)):
+    for k, s in enumerate(_single_step_round(env_id, n, precision, scatter=scatter)):
         assert s["term_mis"] <= max(1, n // 2000) and s["trunc_mis"] <= max(1, n // 2000), s
         ok = s["flags_ok"]
         g_fobs, g_obs, o_fobs, both_done = s["obs"]
@@ -337,6 +353,37 @@ def test_step_variants_bit_identical(env_id, precision, monkeypatch):
         for t, (a_, b_) in enumerate(zip(ref, outs)):
             for x, y in zip(a_, b_):
                 assert torch.equal(x, y), f"variant {v} differs at step {t}"
+
+
+@pytest.mark.parametrize("precision", ["f32", "f64"])
+def test_step_variants_bit_identical_scattered(precision, monkeypatch):
+    """Variant bit-identity from injected poses spread over the field (far obstacles, envs
+    near walls and corners), where the range-checked lidar paths run."""
+    n = 4096
+    orc = O.OracleVectorEnv("usv-simple", n)
+    orc.reset(list(range(100, 100 + n)))
+    rng = np.random.default_rng(11)
+    _scatter(orc.env, rng)
+    far = np.zeros(n, bool)
+    for i in range(n):
+        m = orc.env.n_obs[i]
+        d = np.hypot(orc.env.ox[i, :m] - orc.env.position[i, 0], orc.env.oy[i, :m] - orc.env.position[i, 1])
+        far[i] = (d >= 99).any()
+    assert far.mean() > 0.1, far.mean()          # the far path is actually exercised
+    a = torch.from_numpy(rng.uniform([0.2, -1], [1, 1], size=(n, 2)).astype(np.float32)).cuda()
+    ref = None
+    for v in ("64,0", "16,1", "32,3", "32,5", "32,7", "16,7"):
+        monkeypatch.setenv("USV_STEP_VARIANT", v)
+        env = make("usv-simple", n, seed=3, precision=precision)
+        inject(env, orc.env, elapsed=1)
+        o, r, te, tr, info = env.step(a)
+        out = [x.clone() for x in (o, r, te, tr, info["final_obs"])]
+        env.close()
+        if ref is None:
+            ref = out
+            continue
+        for x, y in zip(ref, out):
+            assert torch.equal(x, y), f"variant {v} differs"
 
 
 # --------------------------------------------------------------------------- usv-asmc-v0 (legacy)

@@ -8,3 +8,4 @@ tail -1 gpurun_out/pytest_gpu_$tag.log
 timeout -k 10 300 python tools/sweep_variants.py --variants "${VARIANTS:-32,3 16,7 32,7 64,7}" 2>/dev/null | grep variant | cut -c1-140
 hipcc -O3 --offload-arch=gfx950 -std=c++17 -fPIC -shared -Iinclude -DUSV_DIAG_STAMPS -o /tmp/libdiag.so gym-usv_amd/csrc/usv_kernels.hip
 USV_LIB_PATH=/tmp/libdiag.so timeout -k 10 120 python tools/stamps.py --variant 32,7 2>/dev/null | python -c "import json,sys; d=json.load(sys.stdin); print({k:(v['mean'] if isinstance(v,dict) else v) for k,v in d.items()})"
+timeout -k 10 300 python tools/workload_stats.py 2>/dev/null
