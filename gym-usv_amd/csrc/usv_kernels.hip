@@ -628,10 +628,13 @@ __device__ __forceinline__ void step_body(const State<R>& S, const IO<R>& io) {
 
   USV_STAMP(0);
   lds_prologue(S, lds, tid);
-  if (tid < kWave) {
-    // ---- phase 1 (wave 0): lane-per-env dynamics; the obs header goes straight to the row
-    if (tid < ne) {
-      const int e = e0 + tid;
+  // The dynamics wave rotates with the block index: the dispatcher places wave w of every block
+  // on SIMD w, so a fixed wave 0 would put all resident blocks' phase 1 on one SIMD.
+  const int dw = blockIdx.x & (kWaves - 1);
+  if (wave == dw) {
+    // ---- phase 1 (one wave): lane-per-env dynamics; the obs header goes straight to the row
+    if (l < ne) {
+      const int e = e0 + l;
       const float2 a = reinterpret_cast<const float2*>(io.act)[e];
       float hdr[kHdr];
       R px, py, sp, cp, partial;
@@ -645,19 +648,20 @@ __device__ __forceinline__ void step_body(const State<R>& S, const IO<R>& io) {
       float* row = io.obs + (size_t)e * kObsDim;
 #pragma unroll
       for (int i = 0; i < kHdr; ++i) row[i] = hdr[i];
-      sh.px[tid] = px; sh.py[tid] = py; sh.sp[tid] = sp; sh.cp[tid] = cp;
-      sh.partial[tid] = partial;
-      sh.trunc[tid] = trunc;
-      sh.n[tid] = S.I(I_NOBS)[e];
+      sh.px[l] = px; sh.py[l] = py; sh.sp[l] = sp; sh.cp[l] = cp;
+      sh.partial[l] = partial;
+      sh.trunc[l] = trunc;
+      sh.n[l] = S.I(I_NOBS)[e];
     }
-    USV_STAMP(1);
+    USV_STAMP_W(1);
   } else {
-    // ---- phase 1 (waves 1..3): stage this block's obstacle rows in LDS (SoA) meanwhile;
-    // rows k = wave-1, wave+2, ...; four loads in flight before their LDS stores
+    // ---- phase 1 (the other three waves): stage this block's obstacle rows in LDS (SoA)
+    // meanwhile; staging wave sw = 0..2 takes rows sw, sw+3, ...; four loads in flight
+    const int sw = (wave - dw - 1) & (kWaves - 1);
     const R4<R>* src = S.obst + (size_t)e0 * cap + l;
     const R4<R> z{R(0), R(0), R(0), R(0)};
     const bool lane_ok = l < cap;
-    for (int k = wave - 1; k < ne; k += 4 * (kWaves - 1)) {
+    for (int k = sw; k < ne; k += 4 * (kWaves - 1)) {
       const int k1 = k + (kWaves - 1), k2 = k + 2 * (kWaves - 1), k3 = k + 3 * (kWaves - 1);
       const R4<R> b0 = lane_ok ? src[(size_t)k * cap] : z;
       const R4<R> b1 = lane_ok && k1 < ne ? src[(size_t)k1 * cap] : z;

@@ -3,7 +3,7 @@
     hipcc ... -DUSV_DIAG_STAMPS -o /tmp/libdiag.so gym-usv_amd/csrc/usv_kernels.hip
     USV_LIB_PATH=/tmp/libdiag.so python tools/stamps.py [--envs 65536] [--variant 32,7]
 
-Stamps (100 MHz ticks, per block): 0 start, 1 wave-0 phase-1 done, 2 after barrier 1,
+Stamps (100 MHz ticks, per block): 0 start, 1 dynamics-wave phase-1 done, 2 after barrier 1,
 3 wave-0 lidar loop done, 4 wave-0 resets done, 5 after barrier 2, 6 end.  Diagnostic only.
 """
 import argparse
@@ -45,7 +45,7 @@ def main():
     st = buf.reshape(32768, 8)[:nb, :7].astype(np.int64)
     t0 = st[:, 0].min()
     st = (st - t0) * 10 / 1000.0   # us
-    ph = {"phase1 (wave0)": st[:, 1] - st[:, 0], "barrier1 wait": st[:, 2] - st[:, 1],
+    ph = {"phase1 (dyn wave)": st[:, 1] - st[:, 0], "barrier1 wait": st[:, 2] - st[:, 1],
           "lidar loop (wave0)": st[:, 3] - st[:, 2], "resets (wave0)": st[:, 4] - st[:, 3],
           "barrier2 wait": st[:, 5] - st[:, 4], "phase3": st[:, 6] - st[:, 5],
           "block total": st[:, 6] - st[:, 0]}
