@@ -454,9 +454,19 @@ struct WinLds {
   unsigned long long* slot;   // [128] per wave, ~0 between envs
   int* mark;                  // [64]  per wave (cross-lane through LDS: ordered by a wave fence)
   const float2* rayoff;       // [128] block-shared ray offset table
-  const float* lx;            // this env's obstacle row (LDS SoA)
-  const float* ly;
-  const float* lr;
+};
+
+// One env's obstacle row in LDS: SoA planes (block kernel, staged through registers) or the
+// global AoS (x, y, r, r^2) row copied verbatim by LDS-DMA (wave kernel).
+template <typename R> struct RowSoA {
+  const R* x; const R* y; const R* r;
+  __device__ __forceinline__ void get(int j, R& X, R& Y, R& Rr) const { X = x[j]; Y = y[j]; Rr = r[j]; }
+};
+template <typename R> struct RowAoS {
+  const R4<R>* p;
+  __device__ __forceinline__ void get(int j, R& X, R& Y, R& Rr) const {
+    const R4<R> v = p[j]; X = v.x; Y = v.y; Rr = v.z;
+  }
 };
 
 // Inclusive max-scan over the 64 lanes (DPP row scans + row carries); identity -1.
@@ -472,10 +482,10 @@ __device__ __forceinline__ int wave_incl_max(int v) {
   return max(v, l >= 48 ? t2 : l >= 32 ? t1 : l >= 16 ? t0 : -1);
 }
 
-template <bool RANGE_CHECK>
+template <bool RANGE_CHECK, typename Row>
 __device__ __forceinline__ void lidar_window(float dx, float dy, float key, float d, float rr, bool valid,
                                              float px, float py, float sp, float cp, const WinLds& L,
-                                             Scan<float>& out) {
+                                             const Row& row, Scan<float>& out) {
   const int l = lane_id();
   const float c0r = ray_c(cp, sp, (float)kStartC, (float)kStartS);
   const float s0r = ray_s(cp, sp, (float)kStartC, (float)kStartS);
@@ -517,7 +527,9 @@ __device__ __forceinline__ void lidar_window(float dx, float dy, float key, floa
     const int l1 = mj & 255, n1 = (mj >> 8) & 255, l2 = mj >> 16;
     int i = k < n1 ? l1 + k : l2 + (k - n1);
     i = min(max(i, 0), 127);
-    const float gdx = L.lx[jj] - px, gdy = L.ly[jj] - py, gr = L.lr[jj];
+    float gx, gy, gr;
+    row.get(jj, gx, gy, gr);
+    const float gdx = gx - px, gdy = gy - py;
     const float2 cs = L.rayoff[i];
     const float c = ray_c(cp, sp, cs.x, cs.y), s = ray_s(cp, sp, cs.x, cs.y);
     const float proj = fmaf(gdx, c, gdy * s);
@@ -537,41 +549,39 @@ __device__ __forceinline__ void lidar_window(float dx, float dy, float key, floa
   const float2 cs0 = L.rayoff[l], cs1 = L.rayoff[l + 64];
   {
     const float c = ray_c(cp, sp, cs0.x, cs0.y), s = ray_s(cp, sp, cs0.x, cs0.y);
-    const float gdx = L.lx[j0] - px, gdy = L.ly[j0] - py, gr = L.lr[j0];
+    float gx, gy, gr;
+    row.get(j0, gx, gy, gr);
+    const float gdx = gx - px, gdy = gy - py;
     const float proj = fmaf(gdx, c, gdy * s), perp = fmaf(gdx, s, -(gdy * c));
     out.rd0 = v0 != ~0ull ? proj - l_sqrt(fmaf(-perp, perp, gr * gr)) : (float)kSensorMax;
   }
   {
     const float c = ray_c(cp, sp, cs1.x, cs1.y), s = ray_s(cp, sp, cs1.x, cs1.y);
-    const float gdx = L.lx[j1] - px, gdy = L.ly[j1] - py, gr = L.lr[j1];
+    float gx, gy, gr;
+    row.get(j1, gx, gy, gr);
+    const float gdx = gx - px, gdy = gy - py;
     const float proj = fmaf(gdx, c, gdy * s), perp = fmaf(gdx, s, -(gdy * c));
     out.rd1 = v1 != ~0ull ? proj - l_sqrt(fmaf(-perp, perp, gr * gr)) : (float)kSensorMax;
   }
 }
 
-// Obstacle row of one env in LDS (SoA), plus the block-shared tables.
-template <typename R> struct EnvLds {
-  const R* lx;
-  const R* ly;
-  const R* lr;
-};
-
-template <typename R, int LID>
-__device__ __forceinline__ void lidar_wave(const EnvLds<R>& E, int n, R px, R py, R sp, R cp,
+template <typename R, int LID, typename Row>
+__device__ __forceinline__ void lidar_wave(const Row& E, int n, R px, R py, R sp, R cp,
                                            const typename Vec2<R>::T* rayoff, unsigned long long* slot,
                                            int* mark, Scan<R>& out) {
   const int l = lane_id();
   const bool valid = l < n;
-  const R ox = valid ? E.lx[l] : R(0), oy = valid ? E.ly[l] : R(0), rr = valid ? E.lr[l] : R(0);
+  R ox = R(0), oy = R(0), rr = R(0);
+  if (valid) E.get(l, ox, oy, rr);
   const R dx = ox - px, dy = oy - py, r2 = rr * rr;
   const R d = l_sqrt(m_fma(dx, dx, dy * dy));
   const R key = valid ? d - rr : big<R>();                                      // simple_env.py:205-206
   out.term = __ballot(valid & (key < R(kTermDist))) != 0;                       // :334
   out.far = __ballot(valid & (d >= R(0.99 * kSensorMax))) != 0;
   if constexpr (std::is_same<R, float>::value && (LID & kLidWindow) != 0) {
-    const WinLds W{slot, mark, rayoff, E.lx, E.ly, E.lr};
-    if (!out.far) lidar_window<false>(dx, dy, key, d, rr, valid, px, py, sp, cp, W, out);
-    else lidar_window<true>(dx, dy, key, d, rr, valid, px, py, sp, cp, W, out);
+    const WinLds W{slot, mark, rayoff};
+    if (!out.far) lidar_window<false>(dx, dy, key, d, rr, valid, px, py, sp, cp, W, E, out);
+    else lidar_window<true>(dx, dy, key, d, rr, valid, px, py, sp, cp, W, E, out);
     return;
   }
   const auto t0 = rayoff[l], t1 = rayoff[l + 64];
@@ -616,7 +626,7 @@ __device__ __forceinline__ void step_body(const State<R>& S, const IO<R>& io) {
   auto* slots = reinterpret_cast<unsigned long long*>(lds + lds_rayoff_bytes<R>());
   int* marks = reinterpret_cast<int*>(lds + lds_rayoff_bytes<R>() + kLdsSlotBytes);
   const int tid = threadIdx.x;
-  const int wave = tid / kWave;
+  const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);   // wave-uniform (SGPR)
   const int l = lane_id();
   const int e0 = blockIdx.x * EPB;
   const int ne = S.N - e0 < EPB ? S.N - e0 : EPB;   // envs of this block
@@ -688,7 +698,7 @@ __device__ __forceinline__ void step_body(const State<R>& S, const IO<R>& io) {
 #ifdef USV_DIAG_NOLIDAR
     sc.rd0 = sc.rd1 = R(kSensorMax) + lox[k * cap]; sc.term = false; sc.far = false;
 #else
-    lidar_wave<R, LID>(EnvLds<R>{lox + k * cap, loy + k * cap, lor + k * cap}, n, sh.px[k], sh.py[k],
+    lidar_wave<R, LID>(RowSoA<R>{lox + k * cap, loy + k * cap, lor + k * cap}, n, sh.px[k], sh.py[k],
                        sh.sp[k], sh.cp[k], rayoff, wslot, wmark, sc);
 #endif
     const bool done = sc.term || sh.trunc[k];
@@ -732,6 +742,167 @@ __device__ __forceinline__ void step_body(const State<R>& S, const IO<R>& io) {
   USV_STAMP(6);
 }
 
+// --------------------------------------------------------------------------- wave-autonomous step
+// Each wave owns EPW consecutive envs end to end and never waits on the other waves of its
+// block after the prologue: lane-per-env dynamics on lanes 0..EPW-1 (header rows written
+// directly), then the wave-per-env lidar loop with the NEXT env's obstacle row prefetched into
+// registers while the current env's scan runs, then same-step resets, then reward and flags.
+// The obstacle reads spread over the whole kernel instead of arriving as one burst while the
+// block's other waves idle at a barrier, and a wave that finishes early frees its slot at once.
+template <typename R, int EPW> struct WaveScratch {
+  R px[EPW], py[EPW], sp[EPW], cp[EPW], partial[EPW];
+  int n[EPW];
+  float hdr[EPW][kHdr];
+  uint8_t trunc[EPW], term[EPW], coll[EPW];
+};
+// one row buffer: the AoS row copied in 16-B pieces, 64 pieces per DMA wave-instruction
+template <typename R> __host__ __device__ constexpr size_t lds_dma_row_bytes(int cap) {
+  return (((size_t)cap * sizeof(R4<R>) + 1023) / 1024) * 1024;
+}
+template <typename R, int EPW> __host__ __device__ constexpr size_t lds_wave_slice(int cap) {
+  return 2 * lds_dma_row_bytes<R>(cap) + ((sizeof(WaveScratch<R, EPW>) + 15) & ~(size_t)15);
+}
+template <typename R, int EPW> __host__ __device__ size_t lds_wave_bytes(int cap) {
+  return lds_head_bytes<R>() + kWaves * lds_wave_slice<R, EPW>(cap);
+}
+
+// LDS-DMA copy of env row `src` (cap <= 64 AoS obstacles) into the wave-uniform LDS buffer
+// `dst`: lane l moves 16-B piece l (+64 for f64).  Inline asm so hipcc does not track it:
+// the compiler would otherwise drain it with vmcnt(0) at the first LDS read it cannot prove
+// disjoint (the ray table), i.e. inside the scan it is meant to overlap.  Completion is
+// counted by hand: dma_wait() before the buffer is read.
+template <typename R>
+__device__ __forceinline__ void dma_row(const R4<R>* src, R4<R>* dst, int cap) {
+  const int nchunk = cap * (int)(sizeof(R4<R>) / 16);
+  const char* g = reinterpret_cast<const char*>(src);
+  const unsigned d = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)dst);
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(R4<R>) / 16); ++i) {
+    const int c = i * kWave + lane_id();
+    if (c < nchunk) {
+      unsigned keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                   "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                   : "=&s"(keep) : "v"(g + 16 * (size_t)c), "s"(d + 16u * i * kWave) : "memory");
+    }
+  }
+}
+// Wait until at most `n` vector-memory operations are outstanding (gfx9 vmcnt counts loads,
+// LDS-DMA and stores in issue order): everything older than the last n has completed.
+template <int N> __device__ __forceinline__ void vm_wait() {
+  static_assert(N >= 0 && N < 16, "vmcnt field");
+  __builtin_amdgcn_s_waitcnt(0x0F70 | N);     // expcnt 7, lgkmcnt 15: no wait on those
+}
+
+template <typename R, int MODE, int EPW, int LID>
+__device__ __forceinline__ void step_body_wave(const State<R>& S, const IO<R>& io) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  auto* rayoff = reinterpret_cast<typename Vec2<R>::T*>(lds);
+  auto* slots = reinterpret_cast<unsigned long long*>(lds + lds_rayoff_bytes<R>());
+  int* marks = reinterpret_cast<int*>(lds + lds_rayoff_bytes<R>() + kLdsSlotBytes);
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);   // wave-uniform (SGPR)
+  const int l = lane_id();
+  const int cap = S.cap;
+  char* wbase = lds + lds_head_bytes<R>() + wave * lds_wave_slice<R, EPW>(cap);
+  R4<R>* rowbuf0 = reinterpret_cast<R4<R>*>(wbase);
+  R4<R>* rowbuf1 = reinterpret_cast<R4<R>*>(wbase + lds_dma_row_bytes<R>(cap));
+  auto& sh = *reinterpret_cast<WaveScratch<R, EPW>*>(wbase + 2 * lds_dma_row_bytes<R>(cap));
+  const int e0 = (blockIdx.x * kWaves + wave) * EPW;        // this wave's envs: e0 .. e0+ne-1
+  const int ne = max(0, min(EPW, S.N - e0));
+
+  USV_STAMP(0);
+  lds_prologue(S, lds, tid);
+  __syncthreads();                                          // ray table and slots ready
+  if (ne == 0) return;
+  dma_row<R>(S.obst + (size_t)e0 * cap, rowbuf0, cap);      // first row in flight during the dynamics
+
+  // ---- dynamics: lane-per-env
+  bool trunc = false;
+  if (l < ne) {
+    const int e = e0 + l;
+    const float2 a = reinterpret_cast<const float2*>(io.act)[e];
+    float hdr[kHdr];
+    R px, py, sp, cp, partial;
+    env_dynamics<R, MODE>(S, e, a.x, a.y, hdr, px, py, sp, cp, partial, trunc);
+    float* row = io.obs + (size_t)e * kObsDim;
+#pragma unroll
+    for (int i = 0; i < kHdr; ++i) { row[i] = hdr[i]; sh.hdr[l][i] = hdr[i]; }
+    sh.px[l] = px; sh.py[l] = py; sh.sp[l] = sp; sh.cp[l] = cp;
+    sh.partial[l] = partial;
+    sh.n[l] = S.I(I_NOBS)[e];
+    sh.trunc[l] = trunc;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");   // scratch rows are read cross-lane
+  __builtin_amdgcn_wave_barrier();
+  USV_STAMP(1);
+  USV_STAMP(2);
+
+  // ---- lidar + observation rows, one env at a time
+  unsigned long long* wslot = slots + wave * 128;
+  int* wmark = marks + wave * 64;
+  for (int k = 0; k < ne; ++k) {
+    const int e = e0 + k;
+    R4<R>* cur = (k & 1) ? rowbuf1 : rowbuf0;
+    // row k landed: it was issued before the previous env's scan (or before the dynamics),
+    // and at least the two sensor-row stores (or the header stores) were issued after it
+    vm_wait<2>();
+    // row k+1 in flight while row k is scanned (its buffer's readers, env k-1, are done)
+    if (k + 1 < ne) dma_row<R>(S.obst + (size_t)(e + 1) * cap, (k & 1) ? rowbuf0 : rowbuf1, cap);
+    const int n = uniform(sh.n[k]);
+    Scan<R> sc;
+    lidar_wave<R, LID>(RowAoS<R>{cur}, n, sh.px[k], sh.py[k], sh.sp[k], sh.cp[k], rayoff,
+                       wslot, wmark, sc);
+    const bool done = sc.term || sh.trunc[k];
+    const bool coll = __ballot((sc.rd0 < R(kCollDist)) | (sc.rd1 < R(kCollDist))) != 0;  // :153-156
+    if (l == 0) { sh.term[k] = sc.term; sh.coll[k] = coll; }
+    const float s0 = (float)l_norm(sc.rd0), s1 = (float)l_norm(sc.rd1);          // :82-83
+    float* row = io.obs + (size_t)e * kObsDim;
+    row[kHdr + l] = s0;                                        // stale scan is kept by reset
+    row[kHdr + 64 + l] = s1;
+    if (done) {
+      if (io.fobs) {                                           // terminal obs
+        float* f = io.fobs + (size_t)e * kObsDim;
+        f[kHdr + l] = s0;
+        f[kHdr + 64 + l] = s1;
+        if (l < kHdr) f[l] = sh.hdr[k][l];
+      }
+      if (S.autoreset == USV_AUTORESET_SAME_STEP) {
+        S.sensor_last[(size_t)e * kSensors + l] = sc.rd0;
+        S.sensor_last[(size_t)e * kSensors + 64 + l] = sc.rd1;
+      }
+    }
+  }
+  USV_STAMP(3);
+  // same-step autoreset of the done envs (own loop: keeps the lidar loop's registers free)
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");   // lane 0's flags are read by all lanes
+  __builtin_amdgcn_wave_barrier();
+  if (S.autoreset == USV_AUTORESET_SAME_STEP) {
+    for (int k = 0; k < ne; ++k)
+      if (sh.term[k] | sh.trunc[k]) reset_wave<R, MODE>(S, e0 + k, io.obs + (size_t)(e0 + k) * kObsDim);
+  }
+  USV_STAMP(4);
+  USV_STAMP(5);
+  // ---- reward and flags, lane-per-env
+  if (l < ne) {
+    const int e = e0 + l;
+    const R coll = sh.coll[l] ? R(-20) : R(0);                              // simple_env.py:153-156
+    io.rew[e] = coll + sh.partial[l];
+    io.term[e] = sh.term[l];
+    io.trunc[e] = sh.trunc[l];
+  }
+  USV_STAMP(6);
+}
+
+template <typename R, int MODE, int EPW, int LID>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(80), amdgpu_num_vgpr(64)))
+void step_kernel_wave_tight(State<R> S, IO<R> io) { step_body_wave<R, MODE, EPW, LID>(S, io); }
+
+template <typename R, int MODE, int EPW, int LID>
+__global__ __launch_bounds__(kBlock) void step_kernel_wave(State<R> S, IO<R> io) {
+  step_body_wave<R, MODE, EPW, LID>(S, io);
+}
+
 // 8 blocks of 256 threads per CU need <= 64 VGPRs and .sgpr_count <= 80 (MI355X_MICROARCH.md,
 // residency: 800 / (ceil(sgpr/16)*16 + 16) blocks; the occupancy API over-reports in 81..96).
 // The f32 usv-simple body fits; the ASMC and f64 bodies need more registers and run at the
@@ -755,7 +926,7 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(State<R> S, IO<R> io) {
   auto* rayoff = reinterpret_cast<typename Vec2<R>::T*>(lds);
   auto* slots = reinterpret_cast<unsigned long long*>(lds + lds_rayoff_bytes<R>());
   const int tid = threadIdx.x;
-  const int wave = tid / kWave;
+  const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);   // wave-uniform (SGPR)
   const int l = lane_id();
   const int e0 = blockIdx.x * kEPBReset;
   const int ne = S.N - e0 < kEPBReset ? S.N - e0 : kEPBReset;
@@ -780,7 +951,7 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(State<R> S, IO<R> io) {
         wx[l] = o.x; wy[l] = o.y; wr[l] = o.z;
       }
       Scan<R> sc;
-      lidar_wave<R, kLidDefault>(EnvLds<R>{wx, wy, wr}, n, S.F(F_X)[e], S.F(F_Y)[e], sp, cp, rayoff,
+      lidar_wave<R, kLidDefault>(RowSoA<R>{wx, wy, wr}, n, S.F(F_X)[e], S.F(F_Y)[e], sp, cp, rayoff,
                                  slots + wave * 128, marks + wave * 64, sc);
       rd0 = sc.rd0;
       rd1 = sc.rd1;
@@ -993,6 +1164,7 @@ struct Handle {
   usv_config cfg;
   int device;
   int epb = 32, lid = 7;     // step-kernel variant (tuned default; see launch_step)
+  int kind = 0;              // 0 = block kernel (phase-1 wave + barriers), 1 = wave-autonomous
   void* slab = nullptr;
   State<float> sf{};
   State<double> sd{};
@@ -1085,6 +1257,25 @@ void* pick_step(int epb, int lid) {
   return pick_lid<R, MODE, 64>(lid);
 }
 
+template <typename R, int MODE, int EPW>
+void* pick_wave_lid(int lid) {
+  if constexpr (std::is_same<R, float>::value && MODE == USV_MODE_SIMPLE) {
+    if (lid == 0) return (void*)&step_kernel_wave_tight<R, MODE, EPW, 0>;
+    if (lid == 3) return (void*)&step_kernel_wave_tight<R, MODE, EPW, 3>;
+    return (void*)&step_kernel_wave_tight<R, MODE, EPW, 7>;
+  }
+  if (lid == 0) return (void*)&step_kernel_wave<R, MODE, EPW, 0>;
+  if (lid == 3) return (void*)&step_kernel_wave<R, MODE, EPW, 3>;
+  return (void*)&step_kernel_wave<R, MODE, EPW, 7>;
+}
+template <typename R, int MODE>
+void* pick_wave(int epw, int lid, size_t* lds, int cap) {
+  if (epw == 4) { *lds = lds_wave_bytes<R, 4>(cap); return pick_wave_lid<R, MODE, 4>(lid); }
+  if (epw == 16) { *lds = lds_wave_bytes<R, 16>(cap); return pick_wave_lid<R, MODE, 16>(lid); }
+  *lds = lds_wave_bytes<R, 8>(cap);
+  return pick_wave_lid<R, MODE, 8>(lid);
+}
+
 template <typename R>
 int launch_step(Handle* h, State<R>& S, const float* act, float* obs, void* rew, uint8_t* term,
                 uint8_t* trunc, float* fobs, hipStream_t st) {
@@ -1095,11 +1286,19 @@ int launch_step(Handle* h, State<R>& S, const float* act, float* obs, void* rew,
     return USV_OK;
   }
   const int epb = h->epb, lid = h->lid;
-  void* fn = h->cfg.mode == USV_MODE_SIMPLE ? pick_step<R, USV_MODE_SIMPLE>(epb, lid)
-                                            : pick_step<R, USV_MODE_ASMC_SIMPLE>(epb, lid);
+  void* fn;
+  size_t lds;
+  if (h->kind == 1) {
+    fn = h->cfg.mode == USV_MODE_SIMPLE ? pick_wave<R, USV_MODE_SIMPLE>(epb / kWaves, lid, &lds, S.cap)
+                                        : pick_wave<R, USV_MODE_ASMC_SIMPLE>(epb / kWaves, lid, &lds, S.cap);
+  } else {
+    fn = h->cfg.mode == USV_MODE_SIMPLE ? pick_step<R, USV_MODE_SIMPLE>(epb, lid)
+                                        : pick_step<R, USV_MODE_ASMC_SIMPLE>(epb, lid);
+    lds = lds_bytes<R>(epb, S.cap);
+  }
   const dim3 grid((S.N + epb - 1) / epb), block(kBlock);
   void* args[] = {(void*)&S, (void*)&io};
-  HIP_TRY(hipLaunchKernel(fn, grid, block, args, lds_bytes<R>(epb, S.cap), st));
+  HIP_TRY(hipLaunchKernel(fn, grid, block, args, lds, st));
   return USV_OK;
 }
 
@@ -1284,11 +1483,14 @@ int usv_create(const usv_config* cfg, int32_t device, void** out) {
   h->device = device;
   h->lid = cfg->lidar_algo == USV_LIDAR_BRUTE ? (kLidSkip | kLidUnroll2) : (kLidSkip | kLidUnroll2 | kLidWindow);
   if (const char* v = std::getenv("USV_STEP_VARIANT")) {   // "epb,lid" tuning override
-    int epb = 0, lid = 0;
-    if (std::sscanf(v, "%d,%d", &epb, &lid) == 2 && (epb == 16 || epb == 32 || epb == 64) &&
-        lid >= 0 && lid <= 7) {
+    int epb = 0, lid = 0, kind = 0;
+    const int got = std::sscanf(v, "%d,%d,%d", &epb, &lid, &kind);
+    const bool blk_ok = kind == 0 && (epb == 16 || epb == 32 || epb == 64);
+    const bool wave_ok = kind == 1 && (epb == 16 || epb == 32 || epb == 64) && (lid == 0 || lid == 3 || lid == 7);
+    if (got >= 2 && (blk_ok || wave_ok) && lid >= 0 && lid <= 7) {
       h->epb = epb;
       h->lid = lid;
+      h->kind = kind;
     }
   }
   const int rc = cfg->precision == USV_F32 ? carve<float>(h, h->sf) : carve<double>(h, h->sd);
