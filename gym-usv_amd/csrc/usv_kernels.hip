@@ -49,7 +49,7 @@ template <typename R> struct State {
   R* sensor_last;          // [N][128]
   R* asmc;                 // [16][N]
   R* v0;                   // [19][fstride] usv-asmc-v0: last[9], aux[3], target[6], action_last
-  const R* ray_tab;        // [2][128] cos / sin(start + i*res)
+  const R* ray_tab;        // [128][2] (cos, sin)(start + i*res)
   int N, cap, limit, autoreset;
   int fstride;             // elements between fields (>= N, 256-B aligned)
   uint64_t seed, gid0;
@@ -613,7 +613,7 @@ template <typename R>
 __device__ __forceinline__ void lds_prologue(const State<R>& S, char* lds, int tid) {
   auto* rayoff = reinterpret_cast<typename Vec2<R>::T*>(lds);
   auto* slots = reinterpret_cast<unsigned long long*>(lds + lds_rayoff_bytes<R>());
-  if (tid < kSensors) rayoff[tid] = typename Vec2<R>::T{S.ray_tab[tid], S.ray_tab[kSensors + tid]};
+  if (tid < kSensors) rayoff[tid] = typename Vec2<R>::T{S.ray_tab[2 * tid], S.ray_tab[2 * tid + 1]};
   for (int i = tid; i < kWaves * 128; i += kBlock) slots[i] = ~0ull;
 }
 
@@ -743,41 +743,45 @@ __device__ __forceinline__ void step_body(const State<R>& S, const IO<R>& io) {
 }
 
 // --------------------------------------------------------------------------- wave-autonomous step
-// Each wave owns EPW consecutive envs end to end and never waits on the other waves of its
-// block after the prologue: lane-per-env dynamics on lanes 0..EPW-1 (header rows written
-// directly), then the wave-per-env lidar loop with the NEXT env's obstacle row prefetched into
-// registers while the current env's scan runs, then same-step resets, then reward and flags.
-// The obstacle reads spread over the whole kernel instead of arriving as one burst while the
-// block's other waves idle at a barrier, and a wave that finishes early frees its slot at once.
+// Each wave owns EPW consecutive envs end to end and shares nothing with the other waves of
+// its block (no barrier anywhere): lane-per-env dynamics, then the wave-per-env lidar loop
+// with the NEXT env's obstacle row in flight (LDS-DMA) while the current env's scan runs,
+// then same-step resets, then reward and flags.  The obstacle reads spread over the whole
+// kernel instead of arriving as one burst while a block's other waves idle at a barrier, and
+// a wave that finishes frees its SIMD slot at once.
+//
+// LDS slice per wave (16-B aligned pieces):
+//   [pair slots 128 x u64][owner marks 64 x i32][ray table 128 x Vec2][row 0][row 1][scratch]
+// The ray table and the rows arrive by LDS-DMA (lane-linear 16-B pieces: `dma_copy`).
 template <typename R, int EPW> struct WaveScratch {
   R px[EPW], py[EPW], sp[EPW], cp[EPW], partial[EPW];
   int n[EPW];
   float hdr[EPW][kHdr];
   uint8_t trunc[EPW], term[EPW], coll[EPW];
 };
-// one row buffer: the AoS row copied in 16-B pieces, 64 pieces per DMA wave-instruction
-template <typename R> __host__ __device__ constexpr size_t lds_dma_row_bytes(int cap) {
-  return (((size_t)cap * sizeof(R4<R>) + 1023) / 1024) * 1024;
+__host__ __device__ constexpr size_t align16(size_t b) { return (b + 15) & ~(size_t)15; }
+template <typename R> __host__ __device__ constexpr size_t wave_row_bytes(int cap) {
+  return align16((size_t)cap * sizeof(R4<R>));
 }
+template <typename R> __host__ __device__ constexpr size_t wave_tab_bytes() { return kSensors * 2 * sizeof(R); }
 template <typename R, int EPW> __host__ __device__ constexpr size_t lds_wave_slice(int cap) {
-  return 2 * lds_dma_row_bytes<R>(cap) + ((sizeof(WaveScratch<R, EPW>) + 15) & ~(size_t)15);
+  return 128 * 8 + 64 * 4 + wave_tab_bytes<R>() + 2 * wave_row_bytes<R>(cap) + align16(sizeof(WaveScratch<R, EPW>));
 }
 template <typename R, int EPW> __host__ __device__ size_t lds_wave_bytes(int cap) {
-  return lds_head_bytes<R>() + kWaves * lds_wave_slice<R, EPW>(cap);
+  return kWaves * lds_wave_slice<R, EPW>(cap);
 }
 
-// LDS-DMA copy of env row `src` (cap <= 64 AoS obstacles) into the wave-uniform LDS buffer
-// `dst`: lane l moves 16-B piece l (+64 for f64).  Inline asm so hipcc does not track it:
-// the compiler would otherwise drain it with vmcnt(0) at the first LDS read it cannot prove
-// disjoint (the ray table), i.e. inside the scan it is meant to overlap.  Completion is
-// counted by hand: dma_wait() before the buffer is read.
-template <typename R>
-__device__ __forceinline__ void dma_row(const R4<R>* src, R4<R>* dst, int cap) {
-  const int nchunk = cap * (int)(sizeof(R4<R>) / 16);
+// LDS-DMA copy of `bytes` (multiple of 16, <= 2 KiB) from global `src` into the wave-uniform
+// LDS buffer `dst`: lane l moves 16-B piece l (and l + 64).  Inline asm so hipcc does not
+// track it: the compiler would otherwise drain it with vmcnt(0) at the first LDS read it
+// cannot prove disjoint, i.e. inside the scan it is meant to overlap.  Completion is counted
+// by hand (vm_wait) before the buffer is read.
+__device__ __forceinline__ void dma_copy(const void* src, void* dst, int bytes) {
+  const int nchunk = bytes / 16;
   const char* g = reinterpret_cast<const char*>(src);
   const unsigned d = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)dst);
 #pragma unroll
-  for (int i = 0; i < (int)(sizeof(R4<R>) / 16); ++i) {
+  for (int i = 0; i < 2; ++i) {
     const int c = i * kWave + lane_id();
     if (c < nchunk) {
       unsigned keep;
@@ -787,8 +791,8 @@ __device__ __forceinline__ void dma_row(const R4<R>* src, R4<R>* dst, int cap) {
     }
   }
 }
-// Wait until at most `n` vector-memory operations are outstanding (gfx9 vmcnt counts loads,
-// LDS-DMA and stores in issue order): everything older than the last n has completed.
+// Wait until at most N vector-memory operations are outstanding (gfx9 vmcnt counts loads,
+// LDS-DMA and stores in issue order): everything older than the last N has completed.
 template <int N> __device__ __forceinline__ void vm_wait() {
   static_assert(N >= 0 && N < 16, "vmcnt field");
   __builtin_amdgcn_s_waitcnt(0x0F70 | N);     // expcnt 7, lgkmcnt 15: no wait on those
@@ -797,58 +801,71 @@ template <int N> __device__ __forceinline__ void vm_wait() {
 template <typename R, int MODE, int EPW, int LID>
 __device__ __forceinline__ void step_body_wave(const State<R>& S, const IO<R>& io) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  auto* rayoff = reinterpret_cast<typename Vec2<R>::T*>(lds);
-  auto* slots = reinterpret_cast<unsigned long long*>(lds + lds_rayoff_bytes<R>());
-  int* marks = reinterpret_cast<int*>(lds + lds_rayoff_bytes<R>() + kLdsSlotBytes);
-  const int tid = threadIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);   // wave-uniform (SGPR)
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);   // wave-uniform (SGPR)
   const int l = lane_id();
   const int cap = S.cap;
-  char* wbase = lds + lds_head_bytes<R>() + wave * lds_wave_slice<R, EPW>(cap);
-  R4<R>* rowbuf0 = reinterpret_cast<R4<R>*>(wbase);
-  R4<R>* rowbuf1 = reinterpret_cast<R4<R>*>(wbase + lds_dma_row_bytes<R>(cap));
-  auto& sh = *reinterpret_cast<WaveScratch<R, EPW>*>(wbase + 2 * lds_dma_row_bytes<R>(cap));
   const int e0 = (blockIdx.x * kWaves + wave) * EPW;        // this wave's envs: e0 .. e0+ne-1
-  const int ne = max(0, min(EPW, S.N - e0));
+  const int ne = min(EPW, S.N - e0);
+  if (ne <= 0) return;                                      // nothing shared: leave at once
+  char* w = lds + wave * lds_wave_slice<R, EPW>(cap);
+  auto* wslot = reinterpret_cast<unsigned long long*>(w);
+  int* wmark = reinterpret_cast<int*>(w + 128 * 8);
+  auto* rayoff = reinterpret_cast<typename Vec2<R>::T*>(w + 128 * 8 + 64 * 4);
+  R4<R>* rowbuf0 = reinterpret_cast<R4<R>*>(w + 128 * 8 + 64 * 4 + wave_tab_bytes<R>());
+  R4<R>* rowbuf1 = reinterpret_cast<R4<R>*>(reinterpret_cast<char*>(rowbuf0) + wave_row_bytes<R>(cap));
+  auto& sh = *reinterpret_cast<WaveScratch<R, EPW>*>(reinterpret_cast<char*>(rowbuf1) + wave_row_bytes<R>(cap));
+  const int rowb = cap * (int)sizeof(R4<R>);
 
-  USV_STAMP(0);
-  lds_prologue(S, lds, tid);
-  __syncthreads();                                          // ray table and slots ready
-  if (ne == 0) return;
-  dma_row<R>(S.obst + (size_t)e0 * cap, rowbuf0, cap);      // first row in flight during the dynamics
+  USV_STAMP_W(0);
+  // ray table (interleaved c, s) and the first obstacle row in flight during the dynamics
+  dma_copy(S.ray_tab, rayoff, (int)wave_tab_bytes<R>());
+  dma_copy(S.obst + (size_t)e0 * cap, rowbuf0, rowb);
+  wslot[l] = ~0ull;
+  wslot[l + 64] = ~0ull;
 
-  // ---- dynamics: lane-per-env
-  bool trunc = false;
-  if (l < ne) {
-    const int e = e0 + l;
+  // ---- dynamics: lane-per-env on lanes 0..ne-1; lanes >= ne recompute env ne-1 and store the
+  // identical values to the identical addresses (benign) -- no divergent memory operations
+  {
+    const int le = min(l, ne - 1);
+    const int e = e0 + le;
     const float2 a = reinterpret_cast<const float2*>(io.act)[e];
     float hdr[kHdr];
     R px, py, sp, cp, partial;
+    bool trunc;
     env_dynamics<R, MODE>(S, e, a.x, a.y, hdr, px, py, sp, cp, partial, trunc);
     float* row = io.obs + (size_t)e * kObsDim;
 #pragma unroll
-    for (int i = 0; i < kHdr; ++i) { row[i] = hdr[i]; sh.hdr[l][i] = hdr[i]; }
-    sh.px[l] = px; sh.py[l] = py; sh.sp[l] = sp; sh.cp[l] = cp;
-    sh.partial[l] = partial;
-    sh.n[l] = S.I(I_NOBS)[e];
-    sh.trunc[l] = trunc;
+    for (int i = 0; i < kHdr; ++i) { row[i] = hdr[i]; sh.hdr[le][i] = hdr[i]; }
+    sh.px[le] = px; sh.py[le] = py; sh.sp[le] = sp; sh.cp[le] = cp;
+    sh.partial[le] = partial;
+    sh.n[le] = S.I(I_NOBS)[e];
+    sh.trunc[le] = trunc;
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");   // scratch rows are read cross-lane
   __builtin_amdgcn_wave_barrier();
-  USV_STAMP(1);
-  USV_STAMP(2);
+  USV_STAMP_W(1);
+  USV_STAMP_W(2);
 
   // ---- lidar + observation rows, one env at a time
-  unsigned long long* wslot = slots + wave * 128;
-  int* wmark = marks + wave * 64;
   for (int k = 0; k < ne; ++k) {
     const int e = e0 + k;
     R4<R>* cur = (k & 1) ? rowbuf1 : rowbuf0;
-    // row k landed: it was issued before the previous env's scan (or before the dynamics),
-    // and at least the two sensor-row stores (or the header stores) were issued after it
+#ifdef USV_WAVE_PRIO
+    // issue priority falls as the wave progresses: lagging waves catch up, so a SIMD's waves
+    // finish together instead of draining one by one at low occupancy
+    switch ((4 * k) / EPW) {
+      case 0: __builtin_amdgcn_s_setprio(3); break;
+      case 1: __builtin_amdgcn_s_setprio(2); break;
+      case 2: __builtin_amdgcn_s_setprio(1); break;
+      default: __builtin_amdgcn_s_setprio(0); break;
+    }
+#endif
+    // row k (and, at k = 0, the ray table) landed: issued before the previous env's scan or
+    // before the dynamics, and at least two vector-memory ops (the sensor-row stores, or the
+    // header stores) were issued after it
     vm_wait<2>();
     // row k+1 in flight while row k is scanned (its buffer's readers, env k-1, are done)
-    if (k + 1 < ne) dma_row<R>(S.obst + (size_t)(e + 1) * cap, (k & 1) ? rowbuf0 : rowbuf1, cap);
+    if (k + 1 < ne) dma_copy(S.obst + (size_t)(e + 1) * cap, (k & 1) ? rowbuf0 : rowbuf1, rowb);
     const int n = uniform(sh.n[k]);
     Scan<R> sc;
     lidar_wave<R, LID>(RowAoS<R>{cur}, n, sh.px[k], sh.py[k], sh.sp[k], sh.cp[k], rayoff,
@@ -873,16 +890,16 @@ __device__ __forceinline__ void step_body_wave(const State<R>& S, const IO<R>& i
       }
     }
   }
-  USV_STAMP(3);
-  // same-step autoreset of the done envs (own loop: keeps the lidar loop's registers free)
+  USV_STAMP_W(3);
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");   // lane 0's flags are read by all lanes
   __builtin_amdgcn_wave_barrier();
+  // same-step autoreset of the done envs (own loop: keeps the lidar loop's registers free)
   if (S.autoreset == USV_AUTORESET_SAME_STEP) {
     for (int k = 0; k < ne; ++k)
       if (sh.term[k] | sh.trunc[k]) reset_wave<R, MODE>(S, e0 + k, io.obs + (size_t)(e0 + k) * kObsDim);
   }
-  USV_STAMP(4);
-  USV_STAMP(5);
+  USV_STAMP_W(4);
+  USV_STAMP_W(5);
   // ---- reward and flags, lane-per-env
   if (l < ne) {
     const int e = e0 + l;
@@ -891,7 +908,7 @@ __device__ __forceinline__ void step_body_wave(const State<R>& S, const IO<R>& i
     io.term[e] = sh.term[l];
     io.trunc[e] = sh.trunc[l];
   }
-  USV_STAMP(6);
+  USV_STAMP_W(6);
 }
 
 template <typename R, int MODE, int EPW, int LID>
@@ -1215,8 +1232,8 @@ int carve(Handle* h, State<R>& S) {
   const double span = (2.0 / 3.0) * (2.0 * kPi), res = span / kSensors;
   for (int i = 0; i < kSensors; ++i) {
     const double a = -kPi * 2.0 / 3.0 + i * res;
-    ht[i] = (R)std::cos(a);
-    ht[kSensors + i] = (R)std::sin(a);
+    ht[2 * i] = (R)std::cos(a);          // interleaved (c, s): the LDS image, copied verbatim
+    ht[2 * i + 1] = (R)std::sin(a);
   }
   HIP_TRY(hipMemcpy(tab, ht.data(), 2 * kSensors * sizeof(R), hipMemcpyHostToDevice));
   // reference __init__ defaults: max_action = [3, 0, 3] (simple_env.py:32)
