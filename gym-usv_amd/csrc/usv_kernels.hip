@@ -50,6 +50,7 @@ template <typename R> struct State {
   R* asmc;                 // [16][N]
   R* v0;                   // [19][fstride] usv-asmc-v0: last[9], aux[3], target[6], action_last
   const R* ray_tab;        // [128][2] (cos, sin)(start + i*res)
+  R4<R>* pose;             // [N] (x, y, sin psi, cos psi) after the step's dynamics (split step)
   int N, cap, limit, autoreset;
   int fstride;             // elements between fields (>= N, 256-B aligned)
   uint64_t seed, gid0;
@@ -920,6 +921,121 @@ __global__ __launch_bounds__(kBlock) void step_kernel_wave(State<R> S, IO<R> io)
   step_body_wave<R, MODE, EPW, LID>(S, io);
 }
 
+// --------------------------------------------------------------------------- split step
+// Two launches per step.  dyn_kernel: lane-per-env dynamics over full 64-lane waves (state,
+// obs header row, partial reward into rew, TimeLimit/bounds truncation into trunc, and the
+// pose record the scan needs).  scan_kernel: the wave-autonomous lidar of step_body_wave with
+// no dynamics in front -- small EPW, so many small blocks and the hardware dispatcher
+// balances the tail -- then same-step resets and the collision term of the reward.
+template <typename R, int MODE>
+__global__ __launch_bounds__(kBlock) void dyn_kernel(State<R> S, IO<R> io) {
+  const int e = blockIdx.x * kBlock + threadIdx.x;
+  if (e >= S.N) return;
+  const float2 a = reinterpret_cast<const float2*>(io.act)[e];
+  float hdr[kHdr];
+  R px, py, sp, cp, partial;
+  bool trunc;
+  env_dynamics<R, MODE>(S, e, a.x, a.y, hdr, px, py, sp, cp, partial, trunc);
+  float* row = io.obs + (size_t)e * kObsDim;
+#pragma unroll
+  for (int i = 0; i < kHdr; ++i) row[i] = hdr[i];
+  S.pose[e] = R4<R>{px, py, sp, cp};
+  io.rew[e] = partial;
+  io.trunc[e] = trunc;
+}
+
+template <typename R> __host__ __device__ constexpr size_t lds_scan_slice(int cap) {
+  return 128 * 8 + 64 * 4 + wave_tab_bytes<R>() + 2 * wave_row_bytes<R>(cap);
+}
+template <typename R> __host__ __device__ size_t lds_scan_bytes(int cap) { return kWaves * lds_scan_slice<R>(cap); }
+
+template <typename R, int MODE, int EPW, int LID>
+__device__ __forceinline__ void scan_body(const State<R>& S, const IO<R>& io) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);   // wave-uniform (SGPR)
+  const int l = lane_id();
+  const int cap = S.cap;
+  const int e0 = (blockIdx.x * kWaves + wave) * EPW;        // this wave's envs: e0 .. e0+ne-1
+  const int ne = min(EPW, S.N - e0);
+  if (ne <= 0) return;
+  char* w = lds + wave * lds_scan_slice<R>(cap);
+  auto* wslot = reinterpret_cast<unsigned long long*>(w);
+  int* wmark = reinterpret_cast<int*>(w + 128 * 8);
+  auto* rayoff = reinterpret_cast<typename Vec2<R>::T*>(w + 128 * 8 + 64 * 4);
+  R4<R>* rowbuf0 = reinterpret_cast<R4<R>*>(w + 128 * 8 + 64 * 4 + wave_tab_bytes<R>());
+  R4<R>* rowbuf1 = reinterpret_cast<R4<R>*>(reinterpret_cast<char*>(rowbuf0) + wave_row_bytes<R>(cap));
+  const int rowb = cap * (int)sizeof(R4<R>);
+
+  USV_STAMP_W(0);
+  dma_copy(S.ray_tab, rayoff, (int)wave_tab_bytes<R>());
+  dma_copy(S.obst + (size_t)e0 * cap, rowbuf0, rowb);
+  wslot[l] = ~0ull;
+  wslot[l + 64] = ~0ull;
+  // this wave's per-env inputs, lane-per-env (lanes >= ne repeat env ne-1), read once: the
+  // scan loop then issues no vector loads and its counted vm_wait stays exact
+  const int le = min(l, ne - 1);
+  const R4<R> P = S.pose[e0 + le];
+  const int nl = S.I(I_NOBS)[e0 + le];
+  const unsigned trunc_m = (unsigned)__ballot(io.trunc[e0 + le] != 0);
+  unsigned term_m = 0, coll_m = 0;                          // bit k: env e0 + k
+  // ray table, row 0 and the per-env inputs landed (an explicit wait hipcc also accounts for,
+  // so it inserts none of its own inside the loop)
+  vm_wait<0>();
+  USV_STAMP_W(1);
+  for (int k = 0; k < ne; ++k) {
+    const int e = e0 + k;
+    R4<R>* cur = (k & 1) ? rowbuf1 : rowbuf0;
+    // row k landed: the two sensor-row stores of env k-1 were issued after its DMA
+    if (k > 0) vm_wait<2>();
+    if (k + 1 < ne) dma_copy(S.obst + (size_t)(e + 1) * cap, (k & 1) ? rowbuf0 : rowbuf1, rowb);
+    Scan<R> sc;
+    lidar_wave<R, LID>(RowAoS<R>{cur}, __builtin_amdgcn_readlane(nl, k), bcast(P.x, k), bcast(P.y, k),
+                       bcast(P.z, k), bcast(P.w, k), rayoff, wslot, wmark, sc);
+    const bool done = sc.term || ((trunc_m >> k) & 1);
+    const bool coll = __ballot((sc.rd0 < R(kCollDist)) | (sc.rd1 < R(kCollDist))) != 0;  // :153-156
+    term_m |= (unsigned)sc.term << k;
+    coll_m |= (unsigned)coll << k;
+    const float s0 = (float)l_norm(sc.rd0), s1 = (float)l_norm(sc.rd1);          // :82-83
+    float* row = io.obs + (size_t)e * kObsDim;
+    row[kHdr + l] = s0;                                        // stale scan is kept by reset
+    row[kHdr + 64 + l] = s1;
+    if (done) {
+      if (io.fobs) {                                           // terminal obs
+        float* f = io.fobs + (size_t)e * kObsDim;
+        f[kHdr + l] = s0;
+        f[kHdr + 64 + l] = s1;
+        if (l < kHdr) f[l] = row[l];                           // header from dyn_kernel
+      }
+      if (S.autoreset == USV_AUTORESET_SAME_STEP) {
+        S.sensor_last[(size_t)e * kSensors + l] = sc.rd0;
+        S.sensor_last[(size_t)e * kSensors + 64 + l] = sc.rd1;
+      }
+    }
+  }
+  USV_STAMP_W(3);
+  // reward collision term and terminated flag, lane-per-env (before the resets reuse rows)
+  if (l < ne) {
+    const int e = e0 + l;
+    if ((coll_m >> l) & 1) io.rew[e] = R(-20) + io.rew[e];                // simple_env.py:153-156
+    io.term[e] = (term_m >> l) & 1;
+  }
+  // same-step autoreset of the done envs
+  if (S.autoreset == USV_AUTORESET_SAME_STEP) {
+    for (int k = 0; k < ne; ++k)
+      if (((term_m | trunc_m) >> k) & 1) reset_wave<R, MODE>(S, e0 + k, io.obs + (size_t)(e0 + k) * kObsDim);
+  }
+  USV_STAMP_W(6);
+}
+
+template <typename R, int MODE, int EPW, int LID>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(80), amdgpu_num_vgpr(64)))
+void scan_kernel_tight(State<R> S, IO<R> io) { scan_body<R, MODE, EPW, LID>(S, io); }
+
+template <typename R, int MODE, int EPW, int LID>
+__global__ __launch_bounds__(kBlock) void scan_kernel(State<R> S, IO<R> io) {
+  scan_body<R, MODE, EPW, LID>(S, io);
+}
+
 // 8 blocks of 256 threads per CU need <= 64 VGPRs and .sgpr_count <= 80 (MI355X_MICROARCH.md,
 // residency: 800 / (ceil(sgpr/16)*16 + 16) blocks; the occupancy API over-reports in 81..96).
 // The f32 usv-simple body fits; the ASMC and f64 bodies need more registers and run at the
@@ -1207,7 +1323,7 @@ int carve(Handle* h, State<R>& S) {
   const size_t bytes = F_NREAL * stride * sizeof(R) + al(I_NINT * stride * 4) +
                        al(N * cap * sizeof(R4<R>)) + al(N * kSensors * sizeof(R)) +
                        al((size_t)kAsmcN * N * sizeof(R)) + al((size_t)kV0N * stride * sizeof(R)) +
-                       al(2 * kSensors * sizeof(R));
+                       al(2 * kSensors * sizeof(R)) + al(N * sizeof(R4<R>));
   HIP_TRY(hipMalloc(&h->slab, bytes));
   HIP_TRY(hipMemset(h->slab, 0, bytes));
   char* p = (char*)h->slab;
@@ -1221,6 +1337,7 @@ int carve(Handle* h, State<R>& S) {
   S.v0 = (R*)take((size_t)kV0N * stride * sizeof(R));
   R* tab = (R*)take(2 * kSensors * sizeof(R));
   S.ray_tab = tab;
+  S.pose = (R4<R>*)take(N * sizeof(R4<R>));
   S.N = h->cfg.num_envs;
   S.cap = h->cfg.obstacle_cap;
   S.limit = h->cfg.max_episode_steps;
@@ -1293,6 +1410,25 @@ void* pick_wave(int epw, int lid, size_t* lds, int cap) {
   return pick_wave_lid<R, MODE, 8>(lid);
 }
 
+template <typename R, int MODE, int EPW>
+void* pick_scan_lid(int lid) {
+  if constexpr (std::is_same<R, float>::value && MODE == USV_MODE_SIMPLE) {
+    if (lid == 0) return (void*)&scan_kernel_tight<R, MODE, EPW, 0>;
+    if (lid == 3) return (void*)&scan_kernel_tight<R, MODE, EPW, 3>;
+    return (void*)&scan_kernel_tight<R, MODE, EPW, 7>;
+  }
+  if (lid == 0) return (void*)&scan_kernel<R, MODE, EPW, 0>;
+  if (lid == 3) return (void*)&scan_kernel<R, MODE, EPW, 3>;
+  return (void*)&scan_kernel<R, MODE, EPW, 7>;
+}
+template <typename R, int MODE>
+void* pick_scan(int epw, int lid) {
+  if (epw == 1) return pick_scan_lid<R, MODE, 1>(lid);
+  if (epw == 2) return pick_scan_lid<R, MODE, 2>(lid);
+  if (epw == 8) return pick_scan_lid<R, MODE, 8>(lid);
+  return pick_scan_lid<R, MODE, 4>(lid);
+}
+
 template <typename R>
 int launch_step(Handle* h, State<R>& S, const float* act, float* obs, void* rew, uint8_t* term,
                 uint8_t* trunc, float* fobs, hipStream_t st) {
@@ -1305,6 +1441,16 @@ int launch_step(Handle* h, State<R>& S, const float* act, float* obs, void* rew,
   const int epb = h->epb, lid = h->lid;
   void* fn;
   size_t lds;
+  if (h->kind == 2) {                                       // split: dynamics, then scan
+    void* args[] = {(void*)&S, (void*)&io};
+    void* dyn = h->cfg.mode == USV_MODE_SIMPLE ? (void*)&dyn_kernel<R, USV_MODE_SIMPLE>
+                                               : (void*)&dyn_kernel<R, USV_MODE_ASMC_SIMPLE>;
+    HIP_TRY(hipLaunchKernel(dyn, dim3((S.N + kBlock - 1) / kBlock), dim3(kBlock), args, 0, st));
+    fn = h->cfg.mode == USV_MODE_SIMPLE ? pick_scan<R, USV_MODE_SIMPLE>(epb / kWaves, lid)
+                                        : pick_scan<R, USV_MODE_ASMC_SIMPLE>(epb / kWaves, lid);
+    HIP_TRY(hipLaunchKernel(fn, dim3((S.N + epb - 1) / epb), dim3(kBlock), args, lds_scan_bytes<R>(S.cap), st));
+    return USV_OK;
+  }
   if (h->kind == 1) {
     fn = h->cfg.mode == USV_MODE_SIMPLE ? pick_wave<R, USV_MODE_SIMPLE>(epb / kWaves, lid, &lds, S.cap)
                                         : pick_wave<R, USV_MODE_ASMC_SIMPLE>(epb / kWaves, lid, &lds, S.cap);
@@ -1504,7 +1650,8 @@ int usv_create(const usv_config* cfg, int32_t device, void** out) {
     const int got = std::sscanf(v, "%d,%d,%d", &epb, &lid, &kind);
     const bool blk_ok = kind == 0 && (epb == 16 || epb == 32 || epb == 64);
     const bool wave_ok = kind == 1 && (epb == 16 || epb == 32 || epb == 64) && (lid == 0 || lid == 3 || lid == 7);
-    if (got >= 2 && (blk_ok || wave_ok) && lid >= 0 && lid <= 7) {
+    const bool split_ok = kind == 2 && (epb == 4 || epb == 8 || epb == 16 || epb == 32) && (lid == 0 || lid == 3 || lid == 7);
+    if (got >= 2 && (blk_ok || wave_ok || split_ok) && lid >= 0 && lid <= 7) {
       h->epb = epb;
       h->lid = lid;
       h->kind = kind;
