@@ -11,6 +11,12 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+// No implicit a*b+c contraction anywhere in the device code: every fused multiply-add is an
+// explicit m_fma/fmaf.  With contraction left to the backend, the same inlined function can
+// round differently in different kernels (it depends on the surrounding code), and the step
+// kernel variants, the split dynamics kernel and the reset kernel must agree bit for bit.
+#pragma clang fp contract(off)
+
 namespace usv {
 
 // ----------------------------------------------------------------------------- constants

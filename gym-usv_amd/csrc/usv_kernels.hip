@@ -403,10 +403,9 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
   v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, true);   // row_shr:2
   v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, true);   // row_shr:4
   v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, true);   // row_shr:8
-  const int l = lane_id();
-  const int t0 = __builtin_amdgcn_readlane(v, 15), t1 = __builtin_amdgcn_readlane(v, 31);
-  const int t2 = __builtin_amdgcn_readlane(v, 47);
-  return v + (l >= 16 ? t0 : 0) + (l >= 32 ? t1 : 0) + (l >= 48 ? t2 : 0);
+  v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+  v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+  return v;
 }
 
 template <typename R, int LID>
@@ -448,9 +447,12 @@ __device__ __forceinline__ void lidar_brute(R dx, R dy, R r2, R key, R d, R rr, 
 // (conservative: a quarter ray of margin around an upper bound of asin(r/d), pi/2 when the boat is
 // inside it), the (obstacle, ray) pairs are expanded over the lanes (prefix sum; each pair's
 // owner found with LDS start markers and a max-scan), each pair runs the same exact test as
-// the brute loop, and the hit with the smallest (key, index) per ray wins through an LDS
-// ds_min_u64 -- the min-key rule, bit-identical to lidar_brute.  ~100 pair tests per env
-// instead of 128 x n.
+// the brute loop, and the hit with the smallest key per ray wins through an LDS ds_min_u64 on
+// (order-preserving key bits << 32 | hit distance bits) -- the min-key rule, and the winner's
+// reading rides along as the payload.  Bit-identical to lidar_brute except on an exact key tie
+// between two different obstacles (measure zero; brute then takes the lower index, this the
+// nearer hit, and the reference's own argsort tie order is unspecified).  ~50 pair tests per
+// env instead of 128 x n.
 struct WinLds {
   unsigned long long* slot;   // [128] per wave, ~0 between envs
   int* mark;                  // [64]  per wave (cross-lane through LDS: ordered by a wave fence)
@@ -470,17 +472,16 @@ template <typename R> struct RowAoS {
   }
 };
 
-// Inclusive max-scan over the 64 lanes (DPP row scans + row carries); identity -1.
+// Inclusive max-scan over the 64 lanes of non-negative values (DPP row scans + row_bcast
+// carries; identity 0, so bound_ctrl zero-fill folds each step into one v_max_i32_dpp).
 __device__ __forceinline__ int wave_incl_max(int v) {
-  v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x111, 0xF, 0xF, false));   // row_shr:1
-  v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x112, 0xF, 0xF, false));   // row_shr:2
-  v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x114, 0xF, 0xF, false));   // row_shr:4
-  v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x118, 0xF, 0xF, false));   // row_shr:8
-  const int l = lane_id();
-  const int t0 = __builtin_amdgcn_readlane(v, 15);
-  const int t1 = max(t0, __builtin_amdgcn_readlane(v, 31));
-  const int t2 = max(t1, __builtin_amdgcn_readlane(v, 47));
-  return max(v, l >= 48 ? t2 : l >= 32 ? t1 : l >= 16 ? t0 : -1);
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, true));   // row_shr:1
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, true));   // row_shr:2
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, true));   // row_shr:4
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, true));   // row_shr:8
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x142, 0xA, 0xF, false));  // row_bcast:15
+  v = max(v, __builtin_amdgcn_update_dpp(0, v, 0x143, 0xC, 0xF, false));  // row_bcast:31
+  return v;
 }
 
 template <bool RANGE_CHECK, typename Row>
@@ -511,23 +512,23 @@ __device__ __forceinline__ void lidar_window(float dx, float dy, float key, floa
   const int W = __builtin_amdgcn_readlane(incl, 63);
   const int meta = lo1 | (len1 << 8) | (lo2 << 16);
   const unsigned ok = ord_key(key);
-  int carry = -1;
+  int carry = 0;                                      // owner marks are lane + 1; 0 = none
   for (int base = 0; base < W; base += kWave) {       // wave-uniform pass count
     // owner of pair q = base + l: the obstacle whose run of pairs starts at or before q
-    L.mark[l] = -1;
-    if (cnt > 0 && off >= base && off < base + kWave) L.mark[off - base] = l;
+    L.mark[l] = 0;
+    if (cnt > 0 && off >= base && off < base + kWave) L.mark[off - base] = l + 1;
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");   // other lanes' marks must be read
     __builtin_amdgcn_wave_barrier();
-    const int j = max(wave_incl_max(L.mark[l]), carry);
-    carry = __builtin_amdgcn_readlane(j, 63);
+    const int j1 = max(wave_incl_max(L.mark[l]), carry);
+    carry = __builtin_amdgcn_readlane(j1, 63);
+    const int j = j1 - 1;
     const int q = base + l;
     const int jj = j < 0 ? 0 : j;
     const int k = q - __shfl(off, jj, kWave);
     const int mj = __shfl(meta, jj, kWave);
     const unsigned gk = (unsigned)__shfl((int)ok, jj, kWave);
     const int l1 = mj & 255, n1 = (mj >> 8) & 255, l2 = mj >> 16;
-    int i = k < n1 ? l1 + k : l2 + (k - n1);
-    i = min(max(i, 0), 127);
+    const int i = min(max((k < n1 ? l1 : l2 - n1) + k, 0), 127);
     float gx, gy, gr;
     row.get(jj, gx, gy, gr);
     const float gdx = gx - px, gdy = gy - py;
@@ -536,34 +537,19 @@ __device__ __forceinline__ void lidar_window(float dx, float dy, float key, floa
     const float proj = fmaf(gdx, c, gdy * s);
     const float perp = fmaf(gdx, s, -(gdy * c));
     const float delta = fmaf(-perp, perp, gr * gr);
+    const float dist = proj - l_sqrt(delta);                 // reading if this pair wins (:457)
     bool hit = (q < W) & (proj >= 0.0f) & (delta >= 0.0f);
-    if (RANGE_CHECK) hit = hit && (proj - l_sqrt(delta)) < (float)kSensorMax;   // :458
+    if (RANGE_CHECK) hit = hit && dist < (float)kSensorMax;   // :458
     if (hit)
-      atomicMin(&L.slot[i], ((unsigned long long)gk << 32) | (unsigned)jj);
+      atomicMin(&L.slot[i], ((unsigned long long)gk << 32) | __float_as_uint(dist));
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");     // all lanes' ds_min_u64 landed
   __builtin_amdgcn_wave_barrier();
   const unsigned long long v0 = L.slot[l], v1 = L.slot[l + 64];
   L.slot[l] = ~0ull;                                  // re-arm for this wave's next env
   L.slot[l + 64] = ~0ull;
-  const int j0 = (int)(unsigned)v0 & 63, j1 = (int)(unsigned)v1 & 63;
-  const float2 cs0 = L.rayoff[l], cs1 = L.rayoff[l + 64];
-  {
-    const float c = ray_c(cp, sp, cs0.x, cs0.y), s = ray_s(cp, sp, cs0.x, cs0.y);
-    float gx, gy, gr;
-    row.get(j0, gx, gy, gr);
-    const float gdx = gx - px, gdy = gy - py;
-    const float proj = fmaf(gdx, c, gdy * s), perp = fmaf(gdx, s, -(gdy * c));
-    out.rd0 = v0 != ~0ull ? proj - l_sqrt(fmaf(-perp, perp, gr * gr)) : (float)kSensorMax;
-  }
-  {
-    const float c = ray_c(cp, sp, cs1.x, cs1.y), s = ray_s(cp, sp, cs1.x, cs1.y);
-    float gx, gy, gr;
-    row.get(j1, gx, gy, gr);
-    const float gdx = gx - px, gdy = gy - py;
-    const float proj = fmaf(gdx, c, gdy * s), perp = fmaf(gdx, s, -(gdy * c));
-    out.rd1 = v1 != ~0ull ? proj - l_sqrt(fmaf(-perp, perp, gr * gr)) : (float)kSensorMax;
-  }
+  out.rd0 = v0 != ~0ull ? __uint_as_float((unsigned)v0) : (float)kSensorMax;
+  out.rd1 = v1 != ~0ull ? __uint_as_float((unsigned)v1) : (float)kSensorMax;
 }
 
 template <typename R, int LID, typename Row>
