@@ -124,6 +124,9 @@ __device__ __forceinline__ double bcast(double v, int lane) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 __device__ __forceinline__ int uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
+// wave64 ballot of a bool straight from its lane mask (HIP's __ballot(int) round-trips the
+// predicate through a VGPR: v_cndmask + v_cmp_ne per call)
+__device__ __forceinline__ unsigned long long ballot(bool p) { return __builtin_amdgcn_ballot_w64(p); }
 
 template <typename R> struct Bits;
 template <> struct Bits<float> { using T = unsigned int; };

@@ -177,7 +177,7 @@ __device__ __forceinline__ void reset_wave(const State<R>& S, int e, float* row)
   // within 0.5 of the start or the target (:261-268), order kept; none left -> one fallback
   const R ox = R(kBound) * U.u[0], oy = R(kBound) * U.u[1], orad = R(0.15) + R(0.35) * U.u[2];
   const bool keep = (l < n) && !(m_hypot(sx - ox, sy - oy) < R(0.5) || m_hypot(tx - ox, ty - oy) < R(0.5));
-  const unsigned long long ball = __ballot(keep);
+  const unsigned long long ball = ballot(keep);
   int cnt = __popcll(ball);
   const int pos = __builtin_amdgcn_mbcnt_hi((unsigned)(ball >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)ball, 0));
   R4<R>* ob = S.obst + (size_t)e * S.cap;
@@ -422,7 +422,7 @@ __device__ __forceinline__ void lidar_brute(R dx, R dy, R r2, R key, R d, R rr, 
     const bool keep = valid & !blind;
     // stream-compact the kept obstacles (order preserved, so min-key ties still resolve to
     // the lowest original index)
-    const unsigned long long ball = __ballot(keep);
+    const unsigned long long ball = ballot(keep);
     m = __popcll(ball);
     const int pos = __builtin_amdgcn_mbcnt_hi((unsigned)(ball >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)ball, 0));
     const int dst = keep ? pos : 63;               // dropped lanes all land in lane 63 (unused)
@@ -501,10 +501,15 @@ __device__ __forceinline__ void lidar_window(float dx, float dy, float key, floa
   const float x = fminf(rr * __builtin_amdgcn_rcpf(d), 1.0f);
   const float half = inside ? (float)(kPi / 2) + margin
                             : fmaf((float)(kPi / 2 - 1) * x, x * x, x) + margin;
+  // in ray units; the second window is the first shifted by one turn = 2 pi / res = 192 rays
+  // exactly (rounding of the shifted float edges would only move an edge that lies within
+  // ~1e-5 ray of an integer, i.e. well inside the quarter-ray margin)
   const float inv = (float)(1.0 / kRes);
-  const int lo1 = max(0, (int)ceilf((phi - half) * inv)), hi1 = min(127, (int)floorf((phi + half) * inv));
-  const float phi2 = phi + (float)(2 * kPi);
-  const int lo2 = max(0, (int)ceilf((phi2 - half) * inv)), hi2 = min(127, (int)floorf((phi2 + half) * inv));
+  const float pr = phi * inv, hr = half * inv;
+  const int a1 = (int)ceilf(pr - hr), b1 = (int)floorf(pr + hr);
+  static_assert(kSensors * 3 == 2 * 192, "192 rays per turn");
+  const int lo1 = max(0, a1), hi1 = min(127, b1);
+  const int lo2 = max(0, a1 + 192), hi2 = min(127, b1 + 192);
   const int len1 = valid ? max(0, hi1 - lo1 + 1) : 0, len2 = valid ? max(0, hi2 - lo2 + 1) : 0;
   const int cnt = len1 + len2;
   const int incl = wave_incl_scan(cnt);
@@ -552,6 +557,107 @@ __device__ __forceinline__ void lidar_window(float dx, float dy, float key, floa
   out.rd1 = v1 != ~0ull ? __uint_as_float((unsigned)v1) : (float)kSensorMax;
 }
 
+// Two envs per wave (f32 window path, <= 32 obstacles each): lanes 0..31 hold env A's
+// obstacles, lanes 32..63 env B's, both envs' (obstacle, ray) pairs go into ONE expanded list,
+// and each pair takes the pose of its owner's env.  The per-obstacle setup, the scans and the
+// pass overhead are shared by the two envs; each pair runs the identical exact test, so the
+// readings are bit-identical to one-env-per-wave.  Slots [256]: env A rays, then env B rays.
+struct Pose2 { float pxA, pyA, spA, cpA, pxB, pyB, spB, cpB; };    // wave-uniform
+
+template <bool RANGE_CHECK>
+__device__ __forceinline__ void lidar_window2(float dx, float dy, float key, float d, float rr, bool valid,
+                                              float sp, float cp, const Pose2& P, const float4* rows,
+                                              int boff, const WinLds& L, Scan<float>& A, Scan<float>& B) {
+  const int l = lane_id();
+  const float c0r = ray_c(cp, sp, (float)kStartC, (float)kStartS);
+  const float s0r = ray_s(cp, sp, (float)kStartC, (float)kStartS);
+  const float a = dx * c0r + dy * s0r, b = dy * c0r - dx * s0r;
+  const float phi = fast_atan2(b, a);                 // CCW angle from ray 0; ray i at i*res
+  const float margin = (float)(0.25 * kRes);          // see lidar_window
+  const bool inside = d <= rr * 1.001f;
+  const float x = fminf(rr * __builtin_amdgcn_rcpf(d), 1.0f);
+  const float half = inside ? (float)(kPi / 2) + margin
+                            : fmaf((float)(kPi / 2 - 1) * x, x * x, x) + margin;
+  const float inv = (float)(1.0 / kRes);
+  const float pr = phi * inv, hr = half * inv;
+  const int a1 = (int)ceilf(pr - hr), b1 = (int)floorf(pr + hr);
+  const int lo1 = max(0, a1), hi1 = min(127, b1);
+  const int lo2 = max(0, a1 + 192), hi2 = min(127, b1 + 192);
+  const int len1 = valid ? max(0, hi1 - lo1 + 1) : 0, len2 = valid ? max(0, hi2 - lo2 + 1) : 0;
+  const int cnt = len1 + len2;
+  const int incl = wave_incl_scan(cnt);
+  const int off = incl - cnt;
+  const int W = __builtin_amdgcn_readlane(incl, 63);
+  const int meta = lo1 | (len1 << 8) | (lo2 << 16);
+  const unsigned ok = ord_key(key);
+  int carry = 0;                                      // owner marks are lane + 1; 0 = none
+  for (int base = 0; base < W; base += kWave) {       // wave-uniform pass count
+    L.mark[l] = 0;
+    if (cnt > 0 && off >= base && off < base + kWave) L.mark[off - base] = l + 1;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const int j1 = max(wave_incl_max(L.mark[l]), carry);
+    carry = __builtin_amdgcn_readlane(j1, 63);
+    const int jj = max(j1 - 1, 0);
+    const int q = base + l;
+    const int k = q - __shfl(off, jj, kWave);
+    const int mj = __shfl(meta, jj, kWave);
+    const unsigned gk = (unsigned)__shfl((int)ok, jj, kWave);
+    const int l1 = mj & 255, n1 = (mj >> 8) & 255, l2 = mj >> 16;
+    const int i = min(max((k < n1 ? l1 : l2 - n1) + k, 0), 127);
+    const bool ob = jj >= 32;                         // owner's env
+    const float opx = ob ? P.pxB : P.pxA, opy = ob ? P.pyB : P.pyA;
+    const float osp = ob ? P.spB : P.spA, ocp = ob ? P.cpB : P.cpA;
+    const float4 o = rows[jj + (ob ? boff : 0)];
+    const float gdx = o.x - opx, gdy = o.y - opy, gr = o.z;
+    const float2 cs = L.rayoff[i];
+    const float c = ray_c(ocp, osp, cs.x, cs.y), s = ray_s(ocp, osp, cs.x, cs.y);
+    const float proj = fmaf(gdx, c, gdy * s);
+    const float perp = fmaf(gdx, s, -(gdy * c));
+    const float delta = fmaf(-perp, perp, gr * gr);
+    const float dist = proj - l_sqrt(delta);
+    bool hit = (q < W) & (proj >= 0.0f) & (delta >= 0.0f);
+    if (RANGE_CHECK) hit = hit && dist < (float)kSensorMax;   // :458
+    if (hit)
+      atomicMin(&L.slot[(ob ? 128 : 0) + i], ((unsigned long long)gk << 32) | __float_as_uint(dist));
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");     // all lanes' ds_min_u64 landed
+  __builtin_amdgcn_wave_barrier();
+  const unsigned long long a0 = L.slot[l], a1s = L.slot[l + 64];
+  const unsigned long long b0 = L.slot[128 + l], b1s = L.slot[192 + l];
+  L.slot[l] = ~0ull; L.slot[l + 64] = ~0ull;          // re-arm for this wave's next pair
+  L.slot[128 + l] = ~0ull; L.slot[192 + l] = ~0ull;
+  A.rd0 = a0 != ~0ull ? __uint_as_float((unsigned)a0) : (float)kSensorMax;
+  A.rd1 = a1s != ~0ull ? __uint_as_float((unsigned)a1s) : (float)kSensorMax;
+  B.rd0 = b0 != ~0ull ? __uint_as_float((unsigned)b0) : (float)kSensorMax;
+  B.rd1 = b1s != ~0ull ? __uint_as_float((unsigned)b1s) : (float)kSensorMax;
+}
+
+// rows: LDS, env A's row at [0, cap), env B's at [cap, 2 cap); nB = 0 when there is no env B.
+__device__ __forceinline__ void lidar_wave2(const float4* rows, int cap, int nA, int nB, const Pose2& P,
+                                            const float2* rayoff, unsigned long long* slot, int* mark,
+                                            Scan<float>& A, Scan<float>& B) {
+  const int l = lane_id();
+  const bool hb = l >= 32;
+  const int jl = l & 31;
+  const bool valid = jl < (hb ? nB : nA);
+  const float px = hb ? P.pxB : P.pxA, py = hb ? P.pyB : P.pyA;
+  const float sp = hb ? P.spB : P.spA, cp = hb ? P.cpB : P.cpA;
+  float ox = 0.0f, oy = 0.0f, rr = 0.0f;
+  if (valid) { const float4 o = rows[(hb ? cap : 0) + jl]; ox = o.x; oy = o.y; rr = o.z; }
+  const float dx = ox - px, dy = oy - py;
+  const float d = l_sqrt(m_fma(dx, dx, dy * dy));
+  const float key = valid ? d - rr : big<float>();                              // simple_env.py:205-206
+  const unsigned long long tb = ballot(valid & (key < (float)kTermDist));       // :334
+  A.term = (unsigned)tb != 0; B.term = (tb >> 32) != 0;
+  A.far = B.far = false;
+  const bool far = ballot(valid & (d >= (float)(0.99 * kSensorMax))) != 0;
+  const WinLds W{slot, mark, rayoff};
+  const int boff = cap - 32;                          // lane j >= 32 -> row index cap + (j - 32)
+  if (!far) lidar_window2<false>(dx, dy, key, d, rr, valid, sp, cp, P, rows, boff, W, A, B);
+  else lidar_window2<true>(dx, dy, key, d, rr, valid, sp, cp, P, rows, boff, W, A, B);
+}
+
 template <typename R, int LID, typename Row>
 __device__ __forceinline__ void lidar_wave(const Row& E, int n, R px, R py, R sp, R cp,
                                            const typename Vec2<R>::T* rayoff, unsigned long long* slot,
@@ -563,8 +669,8 @@ __device__ __forceinline__ void lidar_wave(const Row& E, int n, R px, R py, R sp
   const R dx = ox - px, dy = oy - py, r2 = rr * rr;
   const R d = l_sqrt(m_fma(dx, dx, dy * dy));
   const R key = valid ? d - rr : big<R>();                                      // simple_env.py:205-206
-  out.term = __ballot(valid & (key < R(kTermDist))) != 0;                       // :334
-  out.far = __ballot(valid & (d >= R(0.99 * kSensorMax))) != 0;
+  out.term = ballot(valid & (key < R(kTermDist))) != 0;                       // :334
+  out.far = ballot(valid & (d >= R(0.99 * kSensorMax))) != 0;
   if constexpr (std::is_same<R, float>::value && (LID & kLidWindow) != 0) {
     const WinLds W{slot, mark, rayoff};
     if (!out.far) lidar_window<false>(dx, dy, key, d, rr, valid, px, py, sp, cp, W, E, out);
@@ -689,7 +795,7 @@ __device__ __forceinline__ void step_body(const State<R>& S, const IO<R>& io) {
                        sh.sp[k], sh.cp[k], rayoff, wslot, wmark, sc);
 #endif
     const bool done = sc.term || sh.trunc[k];
-    const bool coll = __ballot((sc.rd0 < R(kCollDist)) | (sc.rd1 < R(kCollDist))) != 0;  // :153-156
+    const bool coll = ballot((sc.rd0 < R(kCollDist)) | (sc.rd1 < R(kCollDist))) != 0;  // :153-156
     if (l == 0) { sh.term[k] = sc.term; sh.coll[k] = coll; }
     const float s0 = (float)l_norm(sc.rd0), s1 = (float)l_norm(sc.rd1);          // :82-83
     const bool reset_now = done && S.autoreset == USV_AUTORESET_SAME_STEP;
@@ -858,7 +964,7 @@ __device__ __forceinline__ void step_body_wave(const State<R>& S, const IO<R>& i
     lidar_wave<R, LID>(RowAoS<R>{cur}, n, sh.px[k], sh.py[k], sh.sp[k], sh.cp[k], rayoff,
                        wslot, wmark, sc);
     const bool done = sc.term || sh.trunc[k];
-    const bool coll = __ballot((sc.rd0 < R(kCollDist)) | (sc.rd1 < R(kCollDist))) != 0;  // :153-156
+    const bool coll = ballot((sc.rd0 < R(kCollDist)) | (sc.rd1 < R(kCollDist))) != 0;  // :153-156
     if (l == 0) { sh.term[k] = sc.term; sh.coll[k] = coll; }
     const float s0 = (float)l_norm(sc.rd0), s1 = (float)l_norm(sc.rd1);          // :82-83
     float* row = io.obs + (size_t)e * kObsDim;
@@ -930,10 +1036,16 @@ __global__ __launch_bounds__(kBlock) void dyn_kernel(State<R> S, IO<R> io) {
   io.trunc[e] = trunc;
 }
 
-template <typename R> __host__ __device__ constexpr size_t lds_scan_slice(int cap) {
-  return 128 * 8 + 64 * 4 + wave_tab_bytes<R>() + 2 * wave_row_bytes<R>(cap);
+// LDS: [ray table, block-shared][per wave: slots 256 x u64, marks 64 x i32, row buffers 2 x (2 rows)]
+template <typename R> __host__ __device__ constexpr size_t scan_rowbuf_bytes(int cap) {
+  return align16(2 * (size_t)cap * sizeof(R4<R>));
 }
-template <typename R> __host__ __device__ size_t lds_scan_bytes(int cap) { return kWaves * lds_scan_slice<R>(cap); }
+template <typename R> __host__ __device__ constexpr size_t lds_scan_slice(int cap) {
+  return 256 * 8 + 64 * 4 + 2 * scan_rowbuf_bytes<R>(cap);
+}
+template <typename R> __host__ __device__ size_t lds_scan_bytes(int cap) {
+  return wave_tab_bytes<R>() + kWaves * lds_scan_slice<R>(cap);
+}
 
 template <typename R, int MODE, int EPW, int LID>
 __device__ __forceinline__ void scan_body(const State<R>& S, const IO<R>& io) {
@@ -943,45 +1055,43 @@ __device__ __forceinline__ void scan_body(const State<R>& S, const IO<R>& io) {
   const int cap = S.cap;
   const int e0 = (blockIdx.x * kWaves + wave) * EPW;        // this wave's envs: e0 .. e0+ne-1
   const int ne = min(EPW, S.N - e0);
-  if (ne <= 0) return;
-  char* w = lds + wave * lds_scan_slice<R>(cap);
+  auto* rayoff = reinterpret_cast<typename Vec2<R>::T*>(lds);
+  char* w = lds + wave_tab_bytes<R>() + wave * lds_scan_slice<R>(cap);
   auto* wslot = reinterpret_cast<unsigned long long*>(w);
-  int* wmark = reinterpret_cast<int*>(w + 128 * 8);
-  auto* rayoff = reinterpret_cast<typename Vec2<R>::T*>(w + 128 * 8 + 64 * 4);
-  R4<R>* rowbuf0 = reinterpret_cast<R4<R>*>(w + 128 * 8 + 64 * 4 + wave_tab_bytes<R>());
-  R4<R>* rowbuf1 = reinterpret_cast<R4<R>*>(reinterpret_cast<char*>(rowbuf0) + wave_row_bytes<R>(cap));
+  int* wmark = reinterpret_cast<int*>(w + 256 * 8);
+  R4<R>* rowbuf0 = reinterpret_cast<R4<R>*>(w + 256 * 8 + 64 * 4);
+  R4<R>* rowbuf1 = reinterpret_cast<R4<R>*>(reinterpret_cast<char*>(rowbuf0) + scan_rowbuf_bytes<R>(cap));
   const int rowb = cap * (int)sizeof(R4<R>);
+  // two envs per wave-iteration on the f32 window path (<= 32 obstacle lanes per env)
+  const bool pair = std::is_same<R, float>::value && (LID & kLidWindow) != 0 && cap <= 32;
+  const int step = pair ? 2 : 1;
 
   USV_STAMP_W(0);
-  dma_copy(S.ray_tab, rayoff, (int)wave_tab_bytes<R>());
-  dma_copy(S.obst + (size_t)e0 * cap, rowbuf0, rowb);
-  wslot[l] = ~0ull;
-  wslot[l + 64] = ~0ull;
+  if (wave == 0) dma_copy(S.ray_tab, rayoff, (int)wave_tab_bytes<R>());
+  const int le = max(0, min(l, ne - 1));
+  if (ne > 0) dma_copy(S.obst + (size_t)e0 * cap, rowbuf0, min(step, ne) * rowb);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) wslot[i * 64 + l] = ~0ull;
   // this wave's per-env inputs, lane-per-env (lanes >= ne repeat env ne-1), read once: the
   // scan loop then issues no vector loads and its counted vm_wait stays exact
-  const int le = min(l, ne - 1);
-  const R4<R> P = S.pose[e0 + le];
-  const int nl = S.I(I_NOBS)[e0 + le];
-  const unsigned trunc_m = (unsigned)__ballot(io.trunc[e0 + le] != 0);
+  const int ec = max(0, min(e0 + le, S.N - 1));
+  const R4<R> P = S.pose[ec];
+  const int nl = S.I(I_NOBS)[ec];
+  const unsigned trunc_m = (unsigned)ballot(io.trunc[ec] != 0);
   unsigned term_m = 0, coll_m = 0;                          // bit k: env e0 + k
-  // ray table, row 0 and the per-env inputs landed (an explicit wait hipcc also accounts for,
-  // so it inserts none of its own inside the loop)
+  // ray table (wave 0's DMA), row 0 and the per-env inputs landed; then the table is shared
   vm_wait<0>();
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  if (ne <= 0) return;
   USV_STAMP_W(1);
-  for (int k = 0; k < ne; ++k) {
+
+  auto emit = [&](int k, const Scan<R>& sc) {               // outputs of env e0 + k
     const int e = e0 + k;
-    R4<R>* cur = (k & 1) ? rowbuf1 : rowbuf0;
-    // row k landed: the two sensor-row stores of env k-1 were issued after its DMA
-    if (k > 0) vm_wait<2>();
-    if (k + 1 < ne) dma_copy(S.obst + (size_t)(e + 1) * cap, (k & 1) ? rowbuf0 : rowbuf1, rowb);
-    Scan<R> sc;
-    lidar_wave<R, LID>(RowAoS<R>{cur}, __builtin_amdgcn_readlane(nl, k), bcast(P.x, k), bcast(P.y, k),
-                       bcast(P.z, k), bcast(P.w, k), rayoff, wslot, wmark, sc);
     const bool done = sc.term || ((trunc_m >> k) & 1);
-    const bool coll = __ballot((sc.rd0 < R(kCollDist)) | (sc.rd1 < R(kCollDist))) != 0;  // :153-156
+    const bool coll = ballot((sc.rd0 < R(kCollDist)) | (sc.rd1 < R(kCollDist))) != 0;  // :153-156
     term_m |= (unsigned)sc.term << k;
     coll_m |= (unsigned)coll << k;
-    const float s0 = (float)l_norm(sc.rd0), s1 = (float)l_norm(sc.rd1);          // :82-83
+    const float s0 = (float)l_norm(sc.rd0), s1 = (float)l_norm(sc.rd1);        // :82-83
     float* row = io.obs + (size_t)e * kObsDim;
     row[kHdr + l] = s0;                                        // stale scan is kept by reset
     row[kHdr + 64 + l] = s1;
@@ -997,6 +1107,34 @@ __device__ __forceinline__ void scan_body(const State<R>& S, const IO<R>& io) {
         S.sensor_last[(size_t)e * kSensors + 64 + l] = sc.rd1;
       }
     }
+  };
+
+  for (int k = 0; k < ne; k += step) {
+    R4<R>* cur = ((k / step) & 1) ? rowbuf1 : rowbuf0;
+    // rows of this iteration landed: at k > 0 at least the two sensor-row stores of the
+    // previous iteration were issued after their DMA
+    if (k > 0) vm_wait<2>();
+    if (k + step < ne)
+      dma_copy(S.obst + (size_t)(e0 + k + step) * cap, ((k / step) & 1) ? rowbuf0 : rowbuf1,
+               min(step, ne - k - step) * rowb);
+    if constexpr (std::is_same<R, float>::value && (LID & kLidWindow) != 0) {
+      if (pair) {
+        const bool hasB = k + 1 < ne;
+        const int kb = hasB ? k + 1 : k;
+        const Pose2 PP{bcast(P.x, k), bcast(P.y, k), bcast(P.z, k), bcast(P.w, k),
+                       bcast(P.x, kb), bcast(P.y, kb), bcast(P.z, kb), bcast(P.w, kb)};
+        Scan<float> sa, sb;
+        lidar_wave2(reinterpret_cast<const float4*>(cur), cap, __builtin_amdgcn_readlane(nl, k),
+                    hasB ? __builtin_amdgcn_readlane(nl, kb) : 0, PP, rayoff, wslot, wmark, sa, sb);
+        emit(k, sa);
+        if (hasB) emit(k + 1, sb);
+        continue;
+      }
+    }
+    Scan<R> sc;
+    lidar_wave<R, LID>(RowAoS<R>{cur}, __builtin_amdgcn_readlane(nl, k), bcast(P.x, k), bcast(P.y, k),
+                       bcast(P.z, k), bcast(P.w, k), rayoff, wslot, wmark, sc);
+    emit(k, sc);
   }
   USV_STAMP_W(3);
   // reward collision term and terminated flag, lane-per-env (before the resets reuse rows)
