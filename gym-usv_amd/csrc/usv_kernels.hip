@@ -835,33 +835,25 @@ __device__ __forceinline__ void step_body(const State<R>& S, const IO<R>& io) {
   USV_STAMP(6);
 }
 
-// --------------------------------------------------------------------------- wave-autonomous step
-// Each wave owns EPW consecutive envs end to end and shares nothing with the other waves of
-// its block (no barrier anywhere): lane-per-env dynamics, then the wave-per-env lidar loop
-// with the NEXT env's obstacle row in flight (LDS-DMA) while the current env's scan runs,
-// then same-step resets, then reward and flags.  The obstacle reads spread over the whole
-// kernel instead of arriving as one burst while a block's other waves idle at a barrier, and
-// a wave that finishes frees its SIMD slot at once.
+// --------------------------------------------------------------------------- wave-per-env scan
+// Shared by the two fast step kernels (step_kernel_wave: dynamics + scan in one launch;
+// dyn_kernel + scan_kernel: split).  Each wave owns EPW consecutive envs and, after one block
+// barrier that publishes the ray table, shares nothing with the other waves of its block: the
+// wave-per-env lidar loop keeps the NEXT envs' obstacle rows in flight (LDS-DMA) while the
+// current ones are scanned; on the f32 window path two envs share each iteration.
 //
-// LDS slice per wave (16-B aligned pieces):
-//   [pair slots 128 x u64][owner marks 64 x i32][ray table 128 x Vec2][row 0][row 1][scratch]
-// The ray table and the rows arrive by LDS-DMA (lane-linear 16-B pieces: `dma_copy`).
-template <typename R, int EPW> struct WaveScratch {
-  R px[EPW], py[EPW], sp[EPW], cp[EPW], partial[EPW];
-  int n[EPW];
-  float hdr[EPW][kHdr];
-  uint8_t trunc[EPW], term[EPW], coll[EPW];
-};
+// LDS: [ray table 128 x Vec2, block-shared]
+//      [per wave: pair slots 256 x u64 | owner marks 64 x i32 | row buffers 2 x (2 rows)]
 __host__ __device__ constexpr size_t align16(size_t b) { return (b + 15) & ~(size_t)15; }
-template <typename R> __host__ __device__ constexpr size_t wave_row_bytes(int cap) {
-  return align16((size_t)cap * sizeof(R4<R>));
-}
 template <typename R> __host__ __device__ constexpr size_t wave_tab_bytes() { return kSensors * 2 * sizeof(R); }
-template <typename R, int EPW> __host__ __device__ constexpr size_t lds_wave_slice(int cap) {
-  return 128 * 8 + 64 * 4 + wave_tab_bytes<R>() + 2 * wave_row_bytes<R>(cap) + align16(sizeof(WaveScratch<R, EPW>));
+template <typename R> __host__ __device__ constexpr size_t scan_rowbuf_bytes(int cap) {
+  return align16(2 * (size_t)cap * sizeof(R4<R>));
 }
-template <typename R, int EPW> __host__ __device__ size_t lds_wave_bytes(int cap) {
-  return kWaves * lds_wave_slice<R, EPW>(cap);
+template <typename R> __host__ __device__ constexpr size_t lds_scan_slice(int cap) {
+  return 256 * 8 + 64 * 4 + 2 * scan_rowbuf_bytes<R>(cap);
+}
+template <typename R> __host__ __device__ size_t lds_scan_bytes(int cap) {
+  return wave_tab_bytes<R>() + kWaves * lds_scan_slice<R>(cap);
 }
 
 // LDS-DMA copy of `bytes` (multiple of 16, <= 2 KiB) from global `src` into the wave-uniform
@@ -891,82 +883,55 @@ template <int N> __device__ __forceinline__ void vm_wait() {
   __builtin_amdgcn_s_waitcnt(0x0F70 | N);     // expcnt 7, lgkmcnt 15: no wait on those
 }
 
-template <typename R, int MODE, int EPW, int LID>
-__device__ __forceinline__ void step_body_wave(const State<R>& S, const IO<R>& io) {
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);   // wave-uniform (SGPR)
+template <typename R> struct ScanLds {
+  typename Vec2<R>::T* rayoff;
+  unsigned long long* slot;
+  int* mark;
+  R4<R>* row0;
+  R4<R>* row1;
+};
+template <typename R>
+__device__ __forceinline__ ScanLds<R> scan_lds(char* lds, int wave, int cap) {
+  char* w = lds + wave_tab_bytes<R>() + wave * lds_scan_slice<R>(cap);
+  R4<R>* r0 = reinterpret_cast<R4<R>*>(w + 256 * 8 + 64 * 4);
+  return ScanLds<R>{reinterpret_cast<typename Vec2<R>::T*>(lds), reinterpret_cast<unsigned long long*>(w),
+                    reinterpret_cast<int*>(w + 256 * 8), r0,
+                    reinterpret_cast<R4<R>*>(reinterpret_cast<char*>(r0) + scan_rowbuf_bytes<R>(cap))};
+}
+// envs per scan iteration: two on the f32 window path (<= 32 obstacle lanes per env)
+template <typename R, int LID> __device__ __forceinline__ int scan_step(int cap) {
+  return (std::is_same<R, float>::value && (LID & kLidWindow) != 0 && cap <= 32) ? 2 : 1;
+}
+// Issue the prologue DMAs (ray table by wave 0, the first iteration's rows) and arm the slots.
+template <typename R, int LID>
+__device__ __forceinline__ void scan_prologue(const State<R>& S, const ScanLds<R>& L, int wave, int e0, int ne) {
+  const int cap = S.cap;
+  if (wave == 0) dma_copy(S.ray_tab, L.rayoff, (int)wave_tab_bytes<R>());
+  if (ne > 0) dma_copy(S.obst + (size_t)e0 * cap, L.row0, min(scan_step<R, LID>(cap), ne) * cap * (int)sizeof(R4<R>));
+#pragma unroll
+  for (int i = 0; i < 4; ++i) L.slot[i * 64 + lane_id()] = ~0ull;
+}
+
+// The scan loop over this wave's ne envs.  Inputs lane-per-env (lane k = env e0 + k): pose
+// P = (x, y, sin psi, cos psi), obstacle count nl, truncation bits trunc_m.  Writes the sensor
+// half of each obs row, final obs and stale scan of done envs; returns term / collision bits.
+// Precondition: the prologue DMAs have landed and the ray table is published.
+template <typename R, int MODE, int LID>
+__device__ __forceinline__ void scan_envs(const State<R>& S, const IO<R>& io, const ScanLds<R>& L, int e0,
+                                          int ne, const R4<R>& P, int nl, unsigned trunc_m,
+                                          unsigned& term_m, unsigned& coll_m) {
   const int l = lane_id();
   const int cap = S.cap;
-  const int e0 = (blockIdx.x * kWaves + wave) * EPW;        // this wave's envs: e0 .. e0+ne-1
-  const int ne = min(EPW, S.N - e0);
-  if (ne <= 0) return;                                      // nothing shared: leave at once
-  char* w = lds + wave * lds_wave_slice<R, EPW>(cap);
-  auto* wslot = reinterpret_cast<unsigned long long*>(w);
-  int* wmark = reinterpret_cast<int*>(w + 128 * 8);
-  auto* rayoff = reinterpret_cast<typename Vec2<R>::T*>(w + 128 * 8 + 64 * 4);
-  R4<R>* rowbuf0 = reinterpret_cast<R4<R>*>(w + 128 * 8 + 64 * 4 + wave_tab_bytes<R>());
-  R4<R>* rowbuf1 = reinterpret_cast<R4<R>*>(reinterpret_cast<char*>(rowbuf0) + wave_row_bytes<R>(cap));
-  auto& sh = *reinterpret_cast<WaveScratch<R, EPW>*>(reinterpret_cast<char*>(rowbuf1) + wave_row_bytes<R>(cap));
   const int rowb = cap * (int)sizeof(R4<R>);
-
-  USV_STAMP_W(0);
-  // ray table (interleaved c, s) and the first obstacle row in flight during the dynamics
-  dma_copy(S.ray_tab, rayoff, (int)wave_tab_bytes<R>());
-  dma_copy(S.obst + (size_t)e0 * cap, rowbuf0, rowb);
-  wslot[l] = ~0ull;
-  wslot[l + 64] = ~0ull;
-
-  // ---- dynamics: lane-per-env on lanes 0..ne-1; lanes >= ne recompute env ne-1 and store the
-  // identical values to the identical addresses (benign) -- no divergent memory operations
-  {
-    const int le = min(l, ne - 1);
-    const int e = e0 + le;
-    const float2 a = reinterpret_cast<const float2*>(io.act)[e];
-    float hdr[kHdr];
-    R px, py, sp, cp, partial;
-    bool trunc;
-    env_dynamics<R, MODE>(S, e, a.x, a.y, hdr, px, py, sp, cp, partial, trunc);
-    float* row = io.obs + (size_t)e * kObsDim;
-#pragma unroll
-    for (int i = 0; i < kHdr; ++i) { row[i] = hdr[i]; sh.hdr[le][i] = hdr[i]; }
-    sh.px[le] = px; sh.py[le] = py; sh.sp[le] = sp; sh.cp[le] = cp;
-    sh.partial[le] = partial;
-    sh.n[le] = S.I(I_NOBS)[e];
-    sh.trunc[le] = trunc;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");   // scratch rows are read cross-lane
-  __builtin_amdgcn_wave_barrier();
-  USV_STAMP_W(1);
-  USV_STAMP_W(2);
-
-  // ---- lidar + observation rows, one env at a time
-  for (int k = 0; k < ne; ++k) {
+  const int step = scan_step<R, LID>(cap);
+  term_m = 0; coll_m = 0;
+  auto emit = [&](int k, const Scan<R>& sc) {               // outputs of env e0 + k
     const int e = e0 + k;
-    R4<R>* cur = (k & 1) ? rowbuf1 : rowbuf0;
-#ifdef USV_WAVE_PRIO
-    // issue priority falls as the wave progresses: lagging waves catch up, so a SIMD's waves
-    // finish together instead of draining one by one at low occupancy
-    switch ((4 * k) / EPW) {
-      case 0: __builtin_amdgcn_s_setprio(3); break;
-      case 1: __builtin_amdgcn_s_setprio(2); break;
-      case 2: __builtin_amdgcn_s_setprio(1); break;
-      default: __builtin_amdgcn_s_setprio(0); break;
-    }
-#endif
-    // row k (and, at k = 0, the ray table) landed: issued before the previous env's scan or
-    // before the dynamics, and at least two vector-memory ops (the sensor-row stores, or the
-    // header stores) were issued after it
-    vm_wait<2>();
-    // row k+1 in flight while row k is scanned (its buffer's readers, env k-1, are done)
-    if (k + 1 < ne) dma_copy(S.obst + (size_t)(e + 1) * cap, (k & 1) ? rowbuf0 : rowbuf1, rowb);
-    const int n = uniform(sh.n[k]);
-    Scan<R> sc;
-    lidar_wave<R, LID>(RowAoS<R>{cur}, n, sh.px[k], sh.py[k], sh.sp[k], sh.cp[k], rayoff,
-                       wslot, wmark, sc);
-    const bool done = sc.term || sh.trunc[k];
+    const bool done = sc.term || ((trunc_m >> k) & 1);
     const bool coll = ballot((sc.rd0 < R(kCollDist)) | (sc.rd1 < R(kCollDist))) != 0;  // :153-156
-    if (l == 0) { sh.term[k] = sc.term; sh.coll[k] = coll; }
-    const float s0 = (float)l_norm(sc.rd0), s1 = (float)l_norm(sc.rd1);          // :82-83
+    term_m |= (unsigned)sc.term << k;
+    coll_m |= (unsigned)coll << k;
+    const float s0 = (float)l_norm(sc.rd0), s1 = (float)l_norm(sc.rd1);        // :82-83
     float* row = io.obs + (size_t)e * kObsDim;
     row[kHdr + l] = s0;                                        // stale scan is kept by reset
     row[kHdr + 64 + l] = s1;
@@ -975,32 +940,107 @@ __device__ __forceinline__ void step_body_wave(const State<R>& S, const IO<R>& i
         float* f = io.fobs + (size_t)e * kObsDim;
         f[kHdr + l] = s0;
         f[kHdr + 64 + l] = s1;
-        if (l < kHdr) f[l] = sh.hdr[k][l];
+        // header: written earlier by this wave (wave kernel) or by dyn_kernel; a wavefront's
+        // own earlier stores are visible to its later loads
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (l < kHdr) f[l] = row[l];
       }
       if (S.autoreset == USV_AUTORESET_SAME_STEP) {
         S.sensor_last[(size_t)e * kSensors + l] = sc.rd0;
         S.sensor_last[(size_t)e * kSensors + 64 + l] = sc.rd1;
       }
     }
+  };
+  for (int k = 0; k < ne; k += step) {
+    R4<R>* cur = ((k / step) & 1) ? L.row1 : L.row0;
+    // rows of this iteration landed: at k > 0 at least the two sensor-row stores of the
+    // previous iteration were issued after their DMA
+    if (k > 0) vm_wait<2>();
+    if (k + step < ne)
+      dma_copy(S.obst + (size_t)(e0 + k + step) * cap, ((k / step) & 1) ? L.row0 : L.row1,
+               min(step, ne - k - step) * rowb);
+    if constexpr (std::is_same<R, float>::value && (LID & kLidWindow) != 0) {
+      if (step == 2) {
+        const bool hasB = k + 1 < ne;
+        const int kb = hasB ? k + 1 : k;
+        const Pose2 PP{bcast(P.x, k), bcast(P.y, k), bcast(P.z, k), bcast(P.w, k),
+                       bcast(P.x, kb), bcast(P.y, kb), bcast(P.z, kb), bcast(P.w, kb)};
+        Scan<float> sa, sb;
+        lidar_wave2(reinterpret_cast<const float4*>(cur), cap, __builtin_amdgcn_readlane(nl, k),
+                    hasB ? __builtin_amdgcn_readlane(nl, kb) : 0, PP, L.rayoff, L.slot, L.mark, sa, sb);
+        emit(k, sa);
+        if (hasB) emit(k + 1, sb);
+        continue;
+      }
+    }
+    Scan<R> sc;
+    lidar_wave<R, LID>(RowAoS<R>{cur}, __builtin_amdgcn_readlane(nl, k), bcast(P.x, k), bcast(P.y, k),
+                       bcast(P.z, k), bcast(P.w, k), L.rayoff, L.slot, L.mark, sc);
+    emit(k, sc);
   }
-  USV_STAMP_W(3);
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");   // lane 0's flags are read by all lanes
-  __builtin_amdgcn_wave_barrier();
-  // same-step autoreset of the done envs (own loop: keeps the lidar loop's registers free)
-  if (S.autoreset == USV_AUTORESET_SAME_STEP) {
-    for (int k = 0; k < ne; ++k)
-      if (sh.term[k] | sh.trunc[k]) reset_wave<R, MODE>(S, e0 + k, io.obs + (size_t)(e0 + k) * kObsDim);
-  }
-  USV_STAMP_W(4);
-  USV_STAMP_W(5);
-  // ---- reward and flags, lane-per-env
+}
+
+// Epilogue shared by both: terminated flag and collision term of the reward (lane-per-env),
+// then same-step autoreset of the done envs.
+template <typename R, int MODE>
+__device__ __forceinline__ void scan_epilogue(const State<R>& S, const IO<R>& io, int e0, int ne,
+                                              R partial, bool have_partial, unsigned term_m,
+                                              unsigned coll_m, unsigned trunc_m) {
+  const int l = lane_id();
   if (l < ne) {
     const int e = e0 + l;
-    const R coll = sh.coll[l] ? R(-20) : R(0);                              // simple_env.py:153-156
-    io.rew[e] = coll + sh.partial[l];
-    io.term[e] = sh.term[l];
-    io.trunc[e] = sh.trunc[l];
+    const bool coll = (coll_m >> l) & 1;                                     // simple_env.py:153-156
+    if (have_partial) io.rew[e] = coll ? R(-20) + partial : partial;
+    else if (coll) io.rew[e] = R(-20) + io.rew[e];
+    io.term[e] = (term_m >> l) & 1;
+    if (have_partial) io.trunc[e] = (trunc_m >> l) & 1;
   }
+  if (S.autoreset == USV_AUTORESET_SAME_STEP) {
+    for (int k = 0; k < ne; ++k)
+      if (((term_m | trunc_m) >> k) & 1) reset_wave<R, MODE>(S, e0 + k, io.obs + (size_t)(e0 + k) * kObsDim);
+  }
+}
+
+// ---- fused: lane-per-env dynamics of the wave's own envs, then the scan
+template <typename R, int MODE, int EPW, int LID>
+__device__ __forceinline__ void step_body_wave(const State<R>& S, const IO<R>& io) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);   // wave-uniform (SGPR)
+  const int l = lane_id();
+  const int e0 = (blockIdx.x * kWaves + wave) * EPW;        // this wave's envs: e0 .. e0+ne-1
+  const int ne = min(EPW, S.N - e0);
+  const ScanLds<R> L = scan_lds<R>(lds, wave, S.cap);
+  USV_STAMP_W(0);
+  scan_prologue<R, LID>(S, L, wave, e0, ne);
+  // dynamics: lanes 0..ne-1; lanes >= ne recompute env ne-1 and store identical values to the
+  // identical addresses (benign) -- no divergent memory operations, so hipcc's own vmcnt
+  // bookkeeping stays exact around the untracked DMAs
+  R px = R(0), py = R(0), sp = R(0), cp = R(1);
+  R partial = R(0);
+  int nl = 0;
+  bool trunc = false;
+  if (ne > 0) {
+    const int e = e0 + min(l, ne - 1);
+    const float2 a = reinterpret_cast<const float2*>(io.act)[e];
+    float hdr[kHdr];
+    env_dynamics<R, MODE>(S, e, a.x, a.y, hdr, px, py, sp, cp, partial, trunc);
+    float* row = io.obs + (size_t)e * kObsDim;
+#pragma unroll
+    for (int i = 0; i < kHdr; ++i) row[i] = hdr[i];
+    nl = S.I(I_NOBS)[e];
+  }
+  const unsigned trunc_m = (unsigned)ballot(trunc);
+  USV_STAMP_W(1);
+  // prologue DMAs landed (the dynamics' loads and stores were issued after them), then the
+  // barrier publishes wave 0's ray table
+  vm_wait<2>();
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  if (ne <= 0) return;
+  USV_STAMP_W(2);
+  unsigned term_m, coll_m;
+  scan_envs<R, MODE, LID>(S, io, L, e0, ne, R4<R>{px, py, sp, cp}, nl, trunc_m, term_m, coll_m);
+  USV_STAMP_W(3);
+  scan_epilogue<R, MODE>(S, io, e0, ne, partial, true, term_m, coll_m, trunc_m);
   USV_STAMP_W(6);
 }
 
@@ -1013,12 +1053,8 @@ __global__ __launch_bounds__(kBlock) void step_kernel_wave(State<R> S, IO<R> io)
   step_body_wave<R, MODE, EPW, LID>(S, io);
 }
 
-// --------------------------------------------------------------------------- split step
-// Two launches per step.  dyn_kernel: lane-per-env dynamics over full 64-lane waves (state,
-// obs header row, partial reward into rew, TimeLimit/bounds truncation into trunc, and the
-// pose record the scan needs).  scan_kernel: the wave-autonomous lidar of step_body_wave with
-// no dynamics in front -- small EPW, so many small blocks and the hardware dispatcher
-// balances the tail -- then same-step resets and the collision term of the reward.
+// ---- split: dyn_kernel (full-width lane-per-env dynamics: state, obs header, partial reward
+// into rew, truncation into trunc, pose record), then scan_kernel
 template <typename R, int MODE>
 __global__ __launch_bounds__(kBlock) void dyn_kernel(State<R> S, IO<R> io) {
   const int e = blockIdx.x * kBlock + threadIdx.x;
@@ -1036,118 +1072,30 @@ __global__ __launch_bounds__(kBlock) void dyn_kernel(State<R> S, IO<R> io) {
   io.trunc[e] = trunc;
 }
 
-// LDS: [ray table, block-shared][per wave: slots 256 x u64, marks 64 x i32, row buffers 2 x (2 rows)]
-template <typename R> __host__ __device__ constexpr size_t scan_rowbuf_bytes(int cap) {
-  return align16(2 * (size_t)cap * sizeof(R4<R>));
-}
-template <typename R> __host__ __device__ constexpr size_t lds_scan_slice(int cap) {
-  return 256 * 8 + 64 * 4 + 2 * scan_rowbuf_bytes<R>(cap);
-}
-template <typename R> __host__ __device__ size_t lds_scan_bytes(int cap) {
-  return wave_tab_bytes<R>() + kWaves * lds_scan_slice<R>(cap);
-}
-
 template <typename R, int MODE, int EPW, int LID>
 __device__ __forceinline__ void scan_body(const State<R>& S, const IO<R>& io) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);   // wave-uniform (SGPR)
   const int l = lane_id();
-  const int cap = S.cap;
-  const int e0 = (blockIdx.x * kWaves + wave) * EPW;        // this wave's envs: e0 .. e0+ne-1
+  const int e0 = (blockIdx.x * kWaves + wave) * EPW;
   const int ne = min(EPW, S.N - e0);
-  auto* rayoff = reinterpret_cast<typename Vec2<R>::T*>(lds);
-  char* w = lds + wave_tab_bytes<R>() + wave * lds_scan_slice<R>(cap);
-  auto* wslot = reinterpret_cast<unsigned long long*>(w);
-  int* wmark = reinterpret_cast<int*>(w + 256 * 8);
-  R4<R>* rowbuf0 = reinterpret_cast<R4<R>*>(w + 256 * 8 + 64 * 4);
-  R4<R>* rowbuf1 = reinterpret_cast<R4<R>*>(reinterpret_cast<char*>(rowbuf0) + scan_rowbuf_bytes<R>(cap));
-  const int rowb = cap * (int)sizeof(R4<R>);
-  // two envs per wave-iteration on the f32 window path (<= 32 obstacle lanes per env)
-  const bool pair = std::is_same<R, float>::value && (LID & kLidWindow) != 0 && cap <= 32;
-  const int step = pair ? 2 : 1;
-
+  const ScanLds<R> L = scan_lds<R>(lds, wave, S.cap);
   USV_STAMP_W(0);
-  if (wave == 0) dma_copy(S.ray_tab, rayoff, (int)wave_tab_bytes<R>());
-  const int le = max(0, min(l, ne - 1));
-  if (ne > 0) dma_copy(S.obst + (size_t)e0 * cap, rowbuf0, min(step, ne) * rowb);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) wslot[i * 64 + l] = ~0ull;
-  // this wave's per-env inputs, lane-per-env (lanes >= ne repeat env ne-1), read once: the
-  // scan loop then issues no vector loads and its counted vm_wait stays exact
-  const int ec = max(0, min(e0 + le, S.N - 1));
+  scan_prologue<R, LID>(S, L, wave, e0, ne);
+  // per-env inputs, lane-per-env (lanes >= ne repeat env ne-1), read once: the scan loop then
+  // issues no vector loads and its counted vm_wait stays exact
+  const int ec = max(0, min(e0 + min(l, ne - 1), S.N - 1));
   const R4<R> P = S.pose[ec];
   const int nl = S.I(I_NOBS)[ec];
   const unsigned trunc_m = (unsigned)ballot(io.trunc[ec] != 0);
-  unsigned term_m = 0, coll_m = 0;                          // bit k: env e0 + k
-  // ray table (wave 0's DMA), row 0 and the per-env inputs landed; then the table is shared
   vm_wait<0>();
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   if (ne <= 0) return;
   USV_STAMP_W(1);
-
-  auto emit = [&](int k, const Scan<R>& sc) {               // outputs of env e0 + k
-    const int e = e0 + k;
-    const bool done = sc.term || ((trunc_m >> k) & 1);
-    const bool coll = ballot((sc.rd0 < R(kCollDist)) | (sc.rd1 < R(kCollDist))) != 0;  // :153-156
-    term_m |= (unsigned)sc.term << k;
-    coll_m |= (unsigned)coll << k;
-    const float s0 = (float)l_norm(sc.rd0), s1 = (float)l_norm(sc.rd1);        // :82-83
-    float* row = io.obs + (size_t)e * kObsDim;
-    row[kHdr + l] = s0;                                        // stale scan is kept by reset
-    row[kHdr + 64 + l] = s1;
-    if (done) {
-      if (io.fobs) {                                           // terminal obs
-        float* f = io.fobs + (size_t)e * kObsDim;
-        f[kHdr + l] = s0;
-        f[kHdr + 64 + l] = s1;
-        if (l < kHdr) f[l] = row[l];                           // header from dyn_kernel
-      }
-      if (S.autoreset == USV_AUTORESET_SAME_STEP) {
-        S.sensor_last[(size_t)e * kSensors + l] = sc.rd0;
-        S.sensor_last[(size_t)e * kSensors + 64 + l] = sc.rd1;
-      }
-    }
-  };
-
-  for (int k = 0; k < ne; k += step) {
-    R4<R>* cur = ((k / step) & 1) ? rowbuf1 : rowbuf0;
-    // rows of this iteration landed: at k > 0 at least the two sensor-row stores of the
-    // previous iteration were issued after their DMA
-    if (k > 0) vm_wait<2>();
-    if (k + step < ne)
-      dma_copy(S.obst + (size_t)(e0 + k + step) * cap, ((k / step) & 1) ? rowbuf0 : rowbuf1,
-               min(step, ne - k - step) * rowb);
-    if constexpr (std::is_same<R, float>::value && (LID & kLidWindow) != 0) {
-      if (pair) {
-        const bool hasB = k + 1 < ne;
-        const int kb = hasB ? k + 1 : k;
-        const Pose2 PP{bcast(P.x, k), bcast(P.y, k), bcast(P.z, k), bcast(P.w, k),
-                       bcast(P.x, kb), bcast(P.y, kb), bcast(P.z, kb), bcast(P.w, kb)};
-        Scan<float> sa, sb;
-        lidar_wave2(reinterpret_cast<const float4*>(cur), cap, __builtin_amdgcn_readlane(nl, k),
-                    hasB ? __builtin_amdgcn_readlane(nl, kb) : 0, PP, rayoff, wslot, wmark, sa, sb);
-        emit(k, sa);
-        if (hasB) emit(k + 1, sb);
-        continue;
-      }
-    }
-    Scan<R> sc;
-    lidar_wave<R, LID>(RowAoS<R>{cur}, __builtin_amdgcn_readlane(nl, k), bcast(P.x, k), bcast(P.y, k),
-                       bcast(P.z, k), bcast(P.w, k), rayoff, wslot, wmark, sc);
-    emit(k, sc);
-  }
+  unsigned term_m, coll_m;
+  scan_envs<R, MODE, LID>(S, io, L, e0, ne, P, nl, trunc_m, term_m, coll_m);
   USV_STAMP_W(3);
-  // reward collision term and terminated flag, lane-per-env (before the resets reuse rows)
-  if (l < ne) {
-    const int e = e0 + l;
-    if ((coll_m >> l) & 1) io.rew[e] = R(-20) + io.rew[e];                // simple_env.py:153-156
-    io.term[e] = (term_m >> l) & 1;
-  }
-  // same-step autoreset of the done envs
-  if (S.autoreset == USV_AUTORESET_SAME_STEP) {
-    for (int k = 0; k < ne; ++k)
-      if (((term_m | trunc_m) >> k) & 1) reset_wave<R, MODE>(S, e0 + k, io.obs + (size_t)(e0 + k) * kObsDim);
-  }
+  scan_epilogue<R, MODE>(S, io, e0, ne, R(0), false, term_m, coll_m, trunc_m);
   USV_STAMP_W(6);
 }
 
@@ -1528,9 +1476,9 @@ void* pick_wave_lid(int lid) {
 }
 template <typename R, int MODE>
 void* pick_wave(int epw, int lid, size_t* lds, int cap) {
-  if (epw == 4) { *lds = lds_wave_bytes<R, 4>(cap); return pick_wave_lid<R, MODE, 4>(lid); }
-  if (epw == 16) { *lds = lds_wave_bytes<R, 16>(cap); return pick_wave_lid<R, MODE, 16>(lid); }
-  *lds = lds_wave_bytes<R, 8>(cap);
+  *lds = lds_scan_bytes<R>(cap);
+  if (epw == 4) return pick_wave_lid<R, MODE, 4>(lid);
+  if (epw == 16) return pick_wave_lid<R, MODE, 16>(lid);
   return pick_wave_lid<R, MODE, 8>(lid);
 }
 
