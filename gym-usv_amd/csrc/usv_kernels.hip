@@ -1368,8 +1368,10 @@ const FieldDesc kFields[USV_FIELD_COUNT] = {
 struct Handle {
   usv_config cfg;
   int device;
-  int epb = 32, lid = 7;     // step-kernel variant (tuned default; see launch_step)
-  int kind = 0;              // 0 = block kernel (phase-1 wave + barriers), 1 = wave-autonomous
+  // step-kernel variant (see launch_step; all variants give identical results):
+  //   kind 0 = block kernel (one dynamics wave per block, barriers), 1 = fused wave kernel
+  //   (step_kernel_wave), 2 = split (dyn_kernel + scan_kernel); epb = envs per 256-thread block
+  int epb = 64, lid = 7, kind = 1;
   void* slab = nullptr;
   State<float> sf{};
   State<double> sd{};
@@ -1717,7 +1719,12 @@ int usv_create(const usv_config* cfg, int32_t device, void** out) {
   h->cfg = *cfg;
   h->device = device;
   h->lid = cfg->lidar_algo == USV_LIDAR_BRUTE ? (kLidSkip | kLidUnroll2) : (kLidSkip | kLidUnroll2 | kLidWindow);
-  if (const char* v = std::getenv("USV_STEP_VARIANT")) {   // "epb,lid" tuning override
+  // tuned defaults at 65 536 envs on MI355X (tools/sweep_variants.py, profiles/): usv-simple
+  // runs the fused wave kernel at 16 envs/wave; usv-asmc-simple the split step (its 20-substep
+  // dynamics want full 64-lane waves) at 4 envs/wave
+  if (cfg->mode == USV_MODE_ASMC_SIMPLE) { h->kind = 2; h->epb = 16; }
+  else { h->kind = 1; h->epb = 64; }
+  if (const char* v = std::getenv("USV_STEP_VARIANT")) {   // "epb,lid[,kind]" tuning override
     int epb = 0, lid = 0, kind = 0;
     const int got = std::sscanf(v, "%d,%d,%d", &epb, &lid, &kind);
     const bool blk_ok = kind == 0 && (epb == 16 || epb == 32 || epb == 64);
