@@ -11,9 +11,9 @@ region (inputs resident in HBM).  Multi-GPU: one process per GPU, envs sharded b
 collectives are the barrier and the max-over-ranks of the elapsed time.
 
 Rank 0 prints one JSON line: value = all ranks' env-steps / max-rank time, plus
-  roofline:     algorithmic bytes per launch / mean kernel duration (HIP events around sampled
-                launches on the env's stream) vs 8 TB/s; traffic from the committed rocprofv3
-                PMC summary (profiles/pmc_summary.json) when it matches the workload.
+  roofline:     algorithmic bytes per launch / mean launch duration (HIP events around groups of
+                back-to-back launches on the env's stream) vs 8 TB/s; traffic from the committed
+                rocprofv3 PMC summary (profiles/pmc_summary.json) when it matches the workload.
   cpu_baseline: the CPU oracle (per-env NumPy restatement of the reference step, oracle/) timed
                 on this host's cores for a bounded sample.
 """
@@ -132,7 +132,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-procs", type=int, default=0, help="0 = min(16, available cores)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--event-every", type=int, default=8, help="time every k-th launch with HIP events")
+    ap.add_argument("--event-every", type=int, default=16, help="launches per HIP-event-timed group")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_summary.json"))
     args = ap.parse_args()
 
@@ -179,27 +179,29 @@ def main():
 
     for k in range(W):
         launch(k)
-    n_ev = (K + args.event_every - 1) // args.event_every
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_ev)]
+    # HIP events on the env's stream bracket groups of G back-to-back launches (one event pair
+    # per group; a pair around every single launch would add its own gap to each launch)
+    G = max(1, args.event_every)
+    groups = K // G
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(groups)]
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     for k in range(K):
-        if k % args.event_every == 0:
-            a, b = ev[k // args.event_every]
-            a.record(stream)
-            launch(W + k)
-            b.record(stream)
-        else:
-            launch(W + k)
+        g, r = divmod(k, G)
+        if g < groups and r == 0:
+            ev[g][0].record(stream)
+        launch(W + k)
+        if g < groups and r == G - 1:
+            ev[g][1].record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    kern_ms = sum(a.elapsed_time(b) for a, b in ev) / len(ev)
+    kern_ms = (sum(a.elapsed_time(b) for a, b in ev) / (groups * G)) if groups else elapsed / K * 1e3
     elapsed, kern_ms = reduce_max([elapsed, kern_ms], device=dev)
 
     if rank == 0:

@@ -4,10 +4,11 @@ profiles/pmc_summary.json (read by bench.py for roofline.traffic).
     python tools/pmc_summary.py --kt DIR --fetch DIR --write DIR --key usv-simple/65536/f32/window --round r01
 
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch (TCC_EA0_RDREQ/WRREQ based, include Infinity
-Cache hits).  On gfx950 FETCH_SIZE under-counts wide (16 B/lane) streaming reads by 2x
-(MI355X_MICROARCH.md, HBM section); this kernel's reads are mostly 4-B/lane SoA loads plus
-16-B obstacle rows, so both the raw value and the 2x-corrected upper bound are recorded and the
-raw (lower) one is used.
+Cache hits).  On gfx950 FETCH_SIZE reports exactly half the bytes of a wide (16 B/lane) coalesced
+read, global_load and LDS-DMA alike, while WRITE_SIZE is exact for streaming stores
+(MI355X_MICROARCH.md, HBM section).  The step kernel's reads are dominated by the 16-B/lane
+LDS-DMA of the obstacle rows, so the reported traffic is 2 x FETCH_SIZE + WRITE_SIZE; the raw sum
+is kept alongside.
 """
 import argparse
 import csv
@@ -39,7 +40,7 @@ def main():
     ap.add_argument("--round", default="r01")
     ap.add_argument("--out", default="profiles")
     a = ap.parse_args()
-    stats = [r for r in rows(a.kt, "*kernel_stats.csv")]
+    stats = [r for r in rows(a.kt, "*kernel_stats.csv") if "usv::" in r["Name"]]
     step = [r for r in stats if "step_kernel" in r["Name"]]
     fetch_kib, nf = counter(a.fetch, "FETCH_SIZE")
     write_kib, nw = counter(a.write, "WRITE_SIZE")
@@ -50,15 +51,16 @@ def main():
         "step_kernel_avg_ns": float(step[0]["AverageNs"]) if step else None,
         "fetch_kib_per_launch": fetch_kib, "write_kib_per_launch": write_kib,
         "fetch_samples": nf, "write_samples": nw,
-        "hbm_bytes_per_launch": round((fetch_kib + write_kib) * 1024),
-        "hbm_bytes_per_launch_fetch_x2": round((2 * fetch_kib + write_kib) * 1024),
+        "hbm_bytes_per_launch": round((2 * fetch_kib + write_kib) * 1024),
+        "hbm_bytes_per_launch_raw": round((fetch_kib + write_kib) * 1024),
+        "correction": "2 x FETCH_SIZE (16-B/lane reads, gfx950) + WRITE_SIZE",
     }
     os.makedirs(a.out, exist_ok=True)
     json.dump(summ, open(os.path.join(a.out, f"{a.round}_summary.json"), "w"), indent=1)
     agg_p = os.path.join(a.out, "pmc_summary.json")
     agg = json.load(open(agg_p)) if os.path.exists(agg_p) else {}
     agg[a.key] = {"hbm_bytes_per_launch": summ["hbm_bytes_per_launch"],
-                  "hbm_bytes_per_launch_fetch_x2": summ["hbm_bytes_per_launch_fetch_x2"],
+                  "hbm_bytes_per_launch_raw": summ["hbm_bytes_per_launch_raw"],
                   "step_kernel_avg_ns": summ["step_kernel_avg_ns"], "round": a.round}
     json.dump(agg, open(agg_p, "w"), indent=1)
     print(json.dumps(summ, indent=1))
