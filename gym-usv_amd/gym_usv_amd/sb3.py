@@ -1,0 +1,230 @@
+"""Stable-Baselines3 integration: a ``VecEnv`` over the HIP vector env.
+
+The reference trains with::
+
+    env = make_vec_env(env_id, n_envs=4, vec_env_cls=DummyVecEnv)     # sb3_train_vec.py:67
+    env = VecVideoRecorder(env, ...)                                   # :68-69
+    env = VecFrameStack(env, 5)                                        # :70
+
+i.e. N Python envs stepped one by one, each wrapped in ``Monitor`` (episode stats) and
+``TimeLimit`` (gym_usv/__init__.py:27,33), with DummyVecEnv's same-step autoreset.  The
+counterpart here is one object::
+
+    from gym_usv_amd.sb3 import Sb3VecEnv
+    env = Sb3VecEnv("usv-simple", num_envs=4096, frame_stack=5)
+
+It duck-types ``stable_baselines3.common.vec_env.VecEnv`` (SB3 itself is not importable in this
+image, so it is not subclassed; ``as_sb3()`` subclasses it where SB3 is installed).  Semantics
+restated from SB3 2.x:
+
+* ``step_wait`` -> (obs ndarray, rewards float32 ndarray, dones bool ndarray, infos list);
+* a done env's info holds ``terminal_observation`` (the final obs; frame-stacked when stacking)
+  and ``TimeLimit.truncated`` (truncated and not terminated), as DummyVecEnv + TimeLimit do;
+* ``episode = {"r", "l", "t"}`` in the info of a done env, as ``Monitor`` writes it;
+* ``frame_stack=k`` is ``VecFrameStack(k)`` (channels-last: the newest obs is the last block,
+  a done env's stack is zeroed before the reset obs is pushed), computed on the device.
+
+The step itself stays on the GPU; only the arrays SB3 consumes are copied to the host.
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+import torch
+
+from .spaces import Box
+
+
+class DeviceFrameStack:
+    """``VecFrameStack`` on device tensors (SB3 ``StackedObservations``, channels-last 1-D obs).
+
+    ``buf`` is [N, k*D]; two buffers alternate so the shift is one out-of-place copy."""
+
+    def __init__(self, num_envs, obs_dim, n_stack, device, dtype=torch.float32):
+        self.n, self.d, self.k = num_envs, obs_dim, n_stack
+        self._bufs = [torch.zeros((num_envs, n_stack * obs_dim), device=device, dtype=dtype) for _ in range(2)]
+        self._i = 0
+
+    @property
+    def buf(self):
+        return self._bufs[self._i]
+
+    def reset(self, obs):
+        b = self.buf
+        b.zero_()
+        b[:, -self.d:] = obs
+        return b
+
+    def step(self, obs, done, final_obs=None):
+        """Push `obs`; returns (stacked obs, stacked terminal obs rows of done envs or None)."""
+        old, new = self._bufs[self._i], self._bufs[1 - self._i]
+        d = self.d
+        new[:, :-d] = old[:, d:]                       # np.roll(stacked, -D, axis=-1)
+        term = None
+        if final_obs is not None and bool(done.any()):
+            idx = done.nonzero().flatten()
+            term = torch.cat((new[idx, :-d], final_obs[idx]), dim=1)
+            new[idx] = 0
+        elif bool(done.any()):
+            new[done] = 0
+        new[:, -d:] = obs
+        self._i = 1 - self._i
+        return new, term
+
+
+def _to_gym_box(box):
+    """The env's Box as a gymnasium Box when gymnasium is importable (SB3 checks spaces)."""
+    try:
+        import gymnasium
+        return gymnasium.spaces.Box(low=box.low, high=box.high, shape=box.shape, dtype=box.dtype)
+    except Exception:
+        return box
+
+
+class Sb3VecEnv:
+    """SB3 ``VecEnv`` of ``num_envs`` HIP-stepped USV envs (+ Monitor, TimeLimit, VecFrameStack).
+
+    ``venv`` may be passed instead of ``env_id`` (anything with the ``UsvVectorEnv`` surface:
+    ``num_envs``, ``obs_dim``, ``act_dim``, ``single_*_space``, ``reset(seed=)``, ``step()`` with
+    same-step autoreset and ``info["final_obs"]``)."""
+
+    def __init__(self, env_id="usv-simple", num_envs=4096, frame_stack=0, seed=0, venv=None, **kw):
+        if venv is None:
+            from .vector_env import UsvVectorEnv
+            venv = UsvVectorEnv(env_id, num_envs=num_envs, seed=seed, autoreset=True, **kw)
+        self.venv = venv
+        self.num_envs = venv.num_envs
+        self.render_mode = None
+        d = venv.obs_dim
+        self._stack = DeviceFrameStack(self.num_envs, d, frame_stack, venv.device) if frame_stack else None
+        obs_space = venv.single_observation_space
+        if frame_stack:
+            obs_space = Box(np.tile(obs_space.low, frame_stack), np.tile(obs_space.high, frame_stack),
+                            dtype=np.float32)
+        self.observation_space = _to_gym_box(obs_space)
+        self.action_space = _to_gym_box(venv.single_action_space)
+        self._seed = seed
+        self._actions = None
+        dev = venv.device
+        self._ep_ret = torch.zeros(self.num_envs, dtype=torch.float64, device=dev)
+        self._ep_len = torch.zeros(self.num_envs, dtype=torch.int64, device=dev)
+        self._t0 = time.time()
+
+    # ---------------------------------------------------------------- VecEnv API
+    def reset(self):
+        obs, _ = self.venv.reset(seed=self._seed)
+        self._seed = None                              # SB3: the seed applies to the next reset only
+        self._ep_ret.zero_()
+        self._ep_len.zero_()
+        if self._stack is not None:
+            obs = self._stack.reset(obs)
+        return obs.cpu().numpy()
+
+    def step_async(self, actions):
+        self._actions = actions
+
+    def step_wait(self):
+        a = torch.as_tensor(np.asarray(self._actions, dtype=np.float32), device=self.venv.device)
+        obs, rew, term, trunc, info = self.venv.step(a)
+        done = term | trunc
+        self._ep_ret += rew.to(torch.float64)
+        self._ep_len += 1
+        final = info.get("final_obs")
+        term_stack = None
+        if self._stack is not None:
+            obs, term_stack = self._stack.step(obs, done, final)
+        # host copies (what SB3 consumes)
+        obs_np = obs.cpu().numpy()
+        rew_np = rew.to(torch.float32).cpu().numpy()
+        done_np = done.cpu().numpy()
+        infos = [{} for _ in range(self.num_envs)]
+        if done_np.any():
+            idx = np.flatnonzero(done_np)
+            tidx = torch.as_tensor(idx, device=self.venv.device)
+            term_obs = (term_stack if term_stack is not None else final[tidx]).cpu().numpy()
+            trunc_np = (trunc & ~term)[tidx].cpu().numpy()
+            ret = self._ep_ret[tidx].cpu().numpy()
+            length = self._ep_len[tidx].cpu().numpy()
+            t = round(time.time() - self._t0, 6)
+            for j, i in enumerate(idx):
+                infos[i]["terminal_observation"] = term_obs[j]
+                infos[i]["TimeLimit.truncated"] = bool(trunc_np[j])
+                infos[i]["episode"] = {"r": round(float(ret[j]), 6), "l": int(length[j]), "t": t}
+            self._ep_ret[tidx] = 0
+            self._ep_len[tidx] = 0
+        return obs_np, rew_np, done_np, infos
+
+    def step(self, actions):
+        self.step_async(actions)
+        return self.step_wait()
+
+    def close(self):
+        self.venv.close()
+
+    def seed(self, seed=None):
+        self._seed = seed
+        return [seed] * self.num_envs
+
+    def get_attr(self, attr_name, indices=None):
+        val = getattr(self.venv, attr_name)
+        return [val] * len(self._indices(indices))
+
+    def set_attr(self, attr_name, value, indices=None):
+        setattr(self.venv, attr_name, value)
+
+    def env_method(self, method_name, *args, indices=None, **kwargs):
+        raise NotImplementedError("per-env methods: the envs are one batched GPU object")
+
+    def env_is_wrapped(self, wrapper_class, indices=None):
+        return [False] * len(self._indices(indices))
+
+    def get_images(self):
+        raise NotImplementedError("rendering is out of scope (SURVEY.md §2 #13)")
+
+    def render(self, mode=None):
+        raise NotImplementedError("rendering is out of scope (SURVEY.md §2 #13)")
+
+    def _indices(self, indices):
+        if indices is None:
+            return range(self.num_envs)
+        if isinstance(indices, int):
+            return [indices]
+        return indices
+
+    # ---------------------------------------------------------------- SB3 proper
+    def as_sb3(self):
+        """A real ``stable_baselines3`` VecEnv subclass instance wrapping this one (SB3 needed)."""
+        from stable_baselines3.common.vec_env import VecEnv
+
+        outer = self
+
+        class _Sb3(VecEnv):
+            def __init__(self):
+                super().__init__(outer.num_envs, outer.observation_space, outer.action_space)
+
+            def reset(self):
+                return outer.reset()
+
+            def step_async(self, actions):
+                outer.step_async(actions)
+
+            def step_wait(self):
+                return outer.step_wait()
+
+            def close(self):
+                outer.close()
+
+            def get_attr(self, attr_name, indices=None):
+                return outer.get_attr(attr_name, indices)
+
+            def set_attr(self, attr_name, value, indices=None):
+                outer.set_attr(attr_name, value, indices)
+
+            def env_method(self, method_name, *method_args, indices=None, **method_kwargs):
+                return outer.env_method(method_name, *method_args, indices=indices, **method_kwargs)
+
+            def env_is_wrapped(self, wrapper_class, indices=None):
+                return outer.env_is_wrapped(wrapper_class, indices)
+
+        return _Sb3()

@@ -1,0 +1,159 @@
+"""SB3 VecEnv adapter (gym_usv_amd.sb3): DummyVecEnv + Monitor + TimeLimit + VecFrameStack semantics.
+
+SB3 is not installed here, so the reference semantics are restated in NumPy below from
+stable-baselines3 2.x (StackedObservations.update / reset, Monitor.step, DummyVecEnv.step_wait,
+TimeLimit's "TimeLimit.truncated"); parity against SB3 itself is unpinned.  The CPU test drives
+the adapter with a synthetic vector env (CPU tensors); the GPU test with the HIP env, against its
+own raw outputs.
+"""
+import numpy as np
+import pytest
+import torch
+
+from gym_usv_amd.sb3 import DeviceFrameStack, Sb3VecEnv
+from gym_usv_amd.spaces import Box
+
+
+class NpFrameStack:
+    """StackedObservations, channels-last, 1-D obs (stable_baselines3/common/vec_env/stacked_observations.py)."""
+
+    def __init__(self, n, d, k):
+        self.s = np.zeros((n, k * d), np.float32)
+        self.d = d
+
+    def reset(self, obs):
+        self.s[...] = 0
+        self.s[:, -self.d:] = obs
+        return self.s.copy()
+
+    def update(self, obs, dones, infos):
+        self.s = np.roll(self.s, -self.d, axis=-1)
+        for i, done in enumerate(dones):
+            if done:
+                infos[i]["terminal_observation"] = np.concatenate((self.s[i, :-self.d], infos[i]["terminal_observation"]))
+                self.s[i] = 0
+        self.s[:, -self.d:] = obs
+        return self.s.copy(), infos
+
+
+class FakeVenv:
+    """UsvVectorEnv-shaped synthetic env with scripted obs / rewards / dones (CPU tensors)."""
+
+    def __init__(self, n=16, d=7, T=60, seed=0):
+        rng = np.random.default_rng(seed)
+        self.num_envs, self.obs_dim, self.act_dim = n, d, 2
+        self.device = torch.device("cpu")
+        self.single_observation_space = Box(-1, 1, shape=(d,))
+        self.single_action_space = Box(np.array([0.2, -1]), np.array([1, 1]), shape=(2,))
+        self.obs = rng.standard_normal((T + 1, n, d)).astype(np.float32)
+        self.final = rng.standard_normal((T, n, d)).astype(np.float32)
+        self.rew = rng.standard_normal((T, n)).astype(np.float32)
+        self.term = rng.random((T, n)) < 0.06
+        self.trunc = (rng.random((T, n)) < 0.04) & ~self.term
+        self.t = 0
+
+    def reset(self, seed=None, options=None):
+        self.t = 0
+        return torch.from_numpy(self.obs[0].copy()), {}
+
+    def step(self, a):
+        t = self.t
+        self.t += 1
+        te, tr = torch.from_numpy(self.term[t].copy()), torch.from_numpy(self.trunc[t].copy())
+        return (torch.from_numpy(self.obs[t + 1].copy()), torch.from_numpy(self.rew[t].copy()), te, tr,
+                {"final_obs": torch.from_numpy(self.final[t].copy()), "_final_obs": te | tr})
+
+    def close(self):
+        pass
+
+
+@pytest.mark.parametrize("k", [0, 5])
+def test_sb3_adapter_semantics_cpu(k):
+    T = 60
+    fv = FakeVenv(T=T)
+    env = Sb3VecEnv(venv=fv, frame_stack=k)
+    n, d = fv.num_envs, fv.obs_dim
+    assert env.observation_space.shape == ((k or 1) * d,)
+    obs = env.reset()
+    ref_stack = NpFrameStack(n, d, k) if k else None
+    ref_obs = ref_stack.reset(fv.obs[0]) if k else fv.obs[0]
+    np.testing.assert_array_equal(obs, ref_obs)
+    ep_ret, ep_len = np.zeros(n), np.zeros(n, int)
+    for t in range(T):
+        o, r, dn, infos = env.step(np.zeros((n, 2), np.float32))
+        done = fv.term[t] | fv.trunc[t]
+        ref_infos = [{} for _ in range(n)]
+        ep_ret += fv.rew[t]
+        ep_len += 1
+        for i in np.flatnonzero(done):                        # DummyVecEnv + TimeLimit + Monitor
+            ref_infos[i]["terminal_observation"] = fv.final[t, i]
+            ref_infos[i]["TimeLimit.truncated"] = bool(fv.trunc[t, i] and not fv.term[t, i])
+            ref_infos[i]["episode"] = {"r": round(float(ep_ret[i]), 6), "l": int(ep_len[i])}
+            ep_ret[i], ep_len[i] = 0, 0
+        if k:
+            ref_o, ref_infos = ref_stack.update(fv.obs[t + 1], done, ref_infos)
+        else:
+            ref_o = fv.obs[t + 1]
+        np.testing.assert_array_equal(o, ref_o)
+        np.testing.assert_array_equal(r, fv.rew[t])
+        np.testing.assert_array_equal(dn, done)
+        for i in range(n):
+            assert set(infos[i]) == set(ref_infos[i])
+            if done[i]:
+                np.testing.assert_array_equal(infos[i]["terminal_observation"], ref_infos[i]["terminal_observation"])
+                assert infos[i]["TimeLimit.truncated"] == ref_infos[i]["TimeLimit.truncated"]
+                assert infos[i]["episode"]["l"] == ref_infos[i]["episode"]["l"]
+                assert abs(infos[i]["episode"]["r"] - ref_infos[i]["episode"]["r"]) < 1e-5
+
+
+def test_device_frame_stack_no_final_obs_cpu():
+    fs = DeviceFrameStack(3, 2, 3, torch.device("cpu"))
+    fs.reset(torch.ones(3, 2))
+    out, term = fs.step(torch.full((3, 2), 2.0), torch.tensor([False, True, False]))
+    assert term is None
+    np.testing.assert_array_equal(out[1].numpy(), [0, 0, 0, 0, 2, 2])
+    np.testing.assert_array_equal(out[0].numpy(), [0, 0, 1, 1, 2, 2])
+
+
+@pytest.mark.gpu
+def test_sb3_adapter_gpu_matches_raw_env():
+    """Sb3VecEnv(frame_stack=5) on the HIP env vs the same-seed raw UsvVectorEnv outputs run through
+    the NumPy restatement: identical obs, rewards, dones and infos."""
+    import gym_usv_amd
+    n, T, k = 512, 300, 5
+    env = Sb3VecEnv("usv-simple", num_envs=n, frame_stack=k, seed=11)
+    raw = gym_usv_amd.make_vec("usv-simple", n, seed=11)
+    rng = np.random.default_rng(2)
+    obs = env.reset()
+    o0, _ = raw.reset(seed=11)
+    st = NpFrameStack(n, 143, k)
+    np.testing.assert_array_equal(obs, st.reset(o0.cpu().numpy()))
+    ep_ret, ep_len, n_done = np.zeros(n), np.zeros(n, int), 0
+    for t in range(T):
+        a = rng.uniform([0.2, -1], [1, 1], size=(n, 2)).astype(np.float32)
+        o, r, dn, infos = env.step(a)
+        ro, rr, rte, rtr, rinfo = raw.step(torch.from_numpy(a).cuda())
+        rr, rte, rtr = rr.cpu().numpy(), rte.cpu().numpy(), rtr.cpu().numpy()
+        done = rte | rtr
+        ref_infos = [{} for _ in range(n)]
+        ep_ret += rr
+        ep_len += 1
+        fin = rinfo["final_obs"].cpu().numpy()
+        for i in np.flatnonzero(done):
+            ref_infos[i]["terminal_observation"] = fin[i].copy()
+            ref_infos[i]["TimeLimit.truncated"] = bool(rtr[i] and not rte[i])
+            ref_infos[i]["episode"] = {"l": int(ep_len[i]), "r": float(ep_ret[i])}
+            ep_ret[i], ep_len[i] = 0, 0
+        ref_o, ref_infos = st.update(ro.cpu().numpy(), done, ref_infos)
+        np.testing.assert_array_equal(o, ref_o)
+        np.testing.assert_array_equal(r, rr)
+        np.testing.assert_array_equal(dn, done)
+        for i in np.flatnonzero(done):
+            n_done += 1
+            np.testing.assert_array_equal(infos[i]["terminal_observation"], ref_infos[i]["terminal_observation"])
+            assert infos[i]["TimeLimit.truncated"] == ref_infos[i]["TimeLimit.truncated"]
+            assert infos[i]["episode"]["l"] == ref_infos[i]["episode"]["l"]
+            assert abs(infos[i]["episode"]["r"] - ref_infos[i]["episode"]["r"]) < 1e-3
+    assert n_done > 0
+    env.close()
+    raw.close()
