@@ -96,6 +96,33 @@ __device__ unsigned long long g_stamps[32768 * kStampSlots];
 #define USV_STAMP(i) do {} while (0)
 #define USV_STAMP_W(i) do {} while (0)
 #endif
+// Diagnostic build only (-DUSV_DIAG_PROF): per-wave shader-clock (s_memtime) cycles spent in
+// each part of the wave-per-env scan, read back with usv_diag_prof().  Never in the product.
+#ifdef USV_DIAG_PROF
+constexpr int kProfWaves = 16384, kProfSlots = 8;
+__device__ unsigned long long g_prof[kProfWaves * kProfSlots];
+struct Prof {
+  unsigned long long acc[kProfSlots] = {};
+  unsigned long long t;
+  __device__ Prof() : t(__builtin_amdgcn_s_memtime()) {}
+  __device__ void mark(int i) {
+    const unsigned long long n = __builtin_amdgcn_s_memtime();
+    acc[i] += n - t;
+    t = n;
+  }
+  __device__ void count(int i) { acc[i] += 1; }
+  __device__ void flush(int gw) {
+    if ((threadIdx.x & 63) == 0 && gw < kProfWaves)
+      for (int k = 0; k < kProfSlots; ++k) g_prof[gw * kProfSlots + k] = acc[k];
+  }
+};
+#else
+struct Prof {
+  __device__ void mark(int) {}
+  __device__ void count(int) {}
+  __device__ void flush(int) {}
+};
+#endif
 template <typename R> struct Vec2;
 template <> struct Vec2<float> { using T = float2; };
 template <> struct Vec2<double> { using T = double2; };
@@ -919,7 +946,7 @@ __device__ __forceinline__ void scan_prologue(const State<R>& S, const ScanLds<R
 template <typename R, int MODE, int LID>
 __device__ __forceinline__ void scan_envs(const State<R>& S, const IO<R>& io, const ScanLds<R>& L, int e0,
                                           int ne, const R4<R>& P, int nl, unsigned trunc_m,
-                                          unsigned& term_m, unsigned& coll_m) {
+                                          unsigned& term_m, unsigned& coll_m, Prof& prof) {
   const int l = lane_id();
   const int cap = S.cap;
   const int rowb = cap * (int)sizeof(R4<R>);
@@ -953,12 +980,15 @@ __device__ __forceinline__ void scan_envs(const State<R>& S, const IO<R>& io, co
   };
   for (int k = 0; k < ne; k += step) {
     R4<R>* cur = ((k / step) & 1) ? L.row1 : L.row0;
+    prof.mark(4);
     // rows of this iteration landed: at k > 0 at least the two sensor-row stores of the
     // previous iteration were issued after their DMA
     if (k > 0) vm_wait<2>();
     if (k + step < ne)
       dma_copy(S.obst + (size_t)(e0 + k + step) * cap, ((k / step) & 1) ? L.row0 : L.row1,
                min(step, ne - k - step) * rowb);
+    prof.mark(1);
+    prof.count(7);
     if constexpr (std::is_same<R, float>::value && (LID & kLidWindow) != 0) {
       if (step == 2) {
         const bool hasB = k + 1 < ne;
@@ -968,15 +998,19 @@ __device__ __forceinline__ void scan_envs(const State<R>& S, const IO<R>& io, co
         Scan<float> sa, sb;
         lidar_wave2(reinterpret_cast<const float4*>(cur), cap, __builtin_amdgcn_readlane(nl, k),
                     hasB ? __builtin_amdgcn_readlane(nl, kb) : 0, PP, L.rayoff, L.slot, L.mark, sa, sb);
+        prof.mark(2);
         emit(k, sa);
         if (hasB) emit(k + 1, sb);
+        prof.mark(3);
         continue;
       }
     }
     Scan<R> sc;
     lidar_wave<R, LID>(RowAoS<R>{cur}, __builtin_amdgcn_readlane(nl, k), bcast(P.x, k), bcast(P.y, k),
                        bcast(P.z, k), bcast(P.w, k), L.rayoff, L.slot, L.mark, sc);
+    prof.mark(2);
     emit(k, sc);
+    prof.mark(3);
   }
 }
 
@@ -1010,6 +1044,7 @@ __device__ __forceinline__ void step_body_wave(const State<R>& S, const IO<R>& i
   const int e0 = (blockIdx.x * kWaves + wave) * EPW;        // this wave's envs: e0 .. e0+ne-1
   const int ne = min(EPW, S.N - e0);
   const ScanLds<R> L = scan_lds<R>(lds, wave, S.cap);
+  Prof prof;
   USV_STAMP_W(0);
   scan_prologue<R, LID>(S, L, wave, e0, ne);
   // dynamics: lanes 0..ne-1; lanes >= ne recompute env ne-1 and store identical values to the
@@ -1037,10 +1072,13 @@ __device__ __forceinline__ void step_body_wave(const State<R>& S, const IO<R>& i
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   if (ne <= 0) return;
   USV_STAMP_W(2);
+  prof.mark(0);
   unsigned term_m, coll_m;
-  scan_envs<R, MODE, LID>(S, io, L, e0, ne, R4<R>{px, py, sp, cp}, nl, trunc_m, term_m, coll_m);
+  scan_envs<R, MODE, LID>(S, io, L, e0, ne, R4<R>{px, py, sp, cp}, nl, trunc_m, term_m, coll_m, prof);
   USV_STAMP_W(3);
   scan_epilogue<R, MODE>(S, io, e0, ne, partial, true, term_m, coll_m, trunc_m);
+  prof.mark(5);
+  prof.flush(blockIdx.x * kWaves + wave);
   USV_STAMP_W(6);
 }
 
@@ -1080,6 +1118,7 @@ __device__ __forceinline__ void scan_body(const State<R>& S, const IO<R>& io) {
   const int e0 = (blockIdx.x * kWaves + wave) * EPW;
   const int ne = min(EPW, S.N - e0);
   const ScanLds<R> L = scan_lds<R>(lds, wave, S.cap);
+  Prof prof;
   USV_STAMP_W(0);
   scan_prologue<R, LID>(S, L, wave, e0, ne);
   // per-env inputs, lane-per-env (lanes >= ne repeat env ne-1), read once: the scan loop then
@@ -1092,10 +1131,13 @@ __device__ __forceinline__ void scan_body(const State<R>& S, const IO<R>& io) {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   if (ne <= 0) return;
   USV_STAMP_W(1);
+  prof.mark(0);
   unsigned term_m, coll_m;
-  scan_envs<R, MODE, LID>(S, io, L, e0, ne, P, nl, trunc_m, term_m, coll_m);
+  scan_envs<R, MODE, LID>(S, io, L, e0, ne, P, nl, trunc_m, term_m, coll_m, prof);
   USV_STAMP_W(3);
   scan_epilogue<R, MODE>(S, io, e0, ne, R(0), false, term_m, coll_m, trunc_m);
+  prof.mark(5);
+  prof.flush(blockIdx.x * kWaves + wave);
   USV_STAMP_W(6);
 }
 
@@ -1671,6 +1713,13 @@ extern "C" {
 
 int usv_abi_version(void) { return USV_ABI_VERSION; }
 
+#ifdef USV_DIAG_PROF
+int usv_diag_prof(void* host, size_t bytes) {
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_prof), bytes < sizeof(g_prof) ? bytes : sizeof(g_prof)));
+  return USV_OK;
+}
+#endif
 #ifdef USV_DIAG_STAMPS
 int usv_diag_stamps(void* host, size_t bytes) {
   HIP_TRY(hipDeviceSynchronize());
