@@ -981,9 +981,11 @@ __device__ __forceinline__ void scan_envs(const State<R>& S, const IO<R>& io, co
   for (int k = 0; k < ne; k += step) {
     R4<R>* cur = ((k / step) & 1) ? L.row1 : L.row0;
     prof.mark(4);
-    // rows of this iteration landed: at k > 0 at least the two sensor-row stores of the
-    // previous iteration were issued after their DMA
-    if (k > 0) vm_wait<2>();
+    // rows of this iteration landed: every env of the previous iteration issued its two
+    // sensor-row stores after their DMA (a full pair: four), so all older ops are done
+    if (k > 0) {
+      if (step == 2) vm_wait<4>(); else vm_wait<2>();
+    }
     if (k + step < ne)
       dma_copy(S.obst + (size_t)(e0 + k + step) * cap, ((k / step) & 1) ? L.row0 : L.row1,
                min(step, ne - k - step) * rowb);
