@@ -876,9 +876,8 @@ template <typename R> __host__ __device__ constexpr size_t wave_tab_bytes() { re
 template <typename R> __host__ __device__ constexpr size_t scan_rowbuf_bytes(int cap) {
   return align16(2 * (size_t)cap * sizeof(R4<R>));
 }
-constexpr int kRowBufs = 3;   // obstacle-row buffers per wave: rows prefetched two iterations ahead
 template <typename R> __host__ __device__ constexpr size_t lds_scan_slice(int cap) {
-  return 256 * 8 + 64 * 4 + kRowBufs * scan_rowbuf_bytes<R>(cap);
+  return 256 * 8 + 64 * 4 + 2 * scan_rowbuf_bytes<R>(cap);
 }
 template <typename R> __host__ __device__ size_t lds_scan_bytes(int cap) {
   return wave_tab_bytes<R>() + kWaves * lds_scan_slice<R>(cap);
@@ -915,29 +914,27 @@ template <typename R> struct ScanLds {
   typename Vec2<R>::T* rayoff;
   unsigned long long* slot;
   int* mark;
-  char* rows;                 // kRowBufs buffers of `rowbuf` bytes
-  int rowbuf;
-  __device__ R4<R>* row(int i) const { return reinterpret_cast<R4<R>*>(rows + i * rowbuf); }
+  R4<R>* row0;
+  R4<R>* row1;
 };
 template <typename R>
 __device__ __forceinline__ ScanLds<R> scan_lds(char* lds, int wave, int cap) {
   char* w = lds + wave_tab_bytes<R>() + wave * lds_scan_slice<R>(cap);
+  R4<R>* r0 = reinterpret_cast<R4<R>*>(w + 256 * 8 + 64 * 4);
   return ScanLds<R>{reinterpret_cast<typename Vec2<R>::T*>(lds), reinterpret_cast<unsigned long long*>(w),
-                    reinterpret_cast<int*>(w + 256 * 8), w + 256 * 8 + 64 * 4, (int)scan_rowbuf_bytes<R>(cap)};
+                    reinterpret_cast<int*>(w + 256 * 8), r0,
+                    reinterpret_cast<R4<R>*>(reinterpret_cast<char*>(r0) + scan_rowbuf_bytes<R>(cap))};
 }
 // envs per scan iteration: two on the f32 window path (<= 32 obstacle lanes per env)
 template <typename R, int LID> __device__ __forceinline__ int scan_step(int cap) {
   return (std::is_same<R, float>::value && (LID & kLidWindow) != 0 && cap <= 32) ? 2 : 1;
 }
-// Issue the prologue DMAs (ray table by wave 0, the first two iterations' rows) and arm the slots.
+// Issue the prologue DMAs (ray table by wave 0, the first iteration's rows) and arm the slots.
 template <typename R, int LID>
 __device__ __forceinline__ void scan_prologue(const State<R>& S, const ScanLds<R>& L, int wave, int e0, int ne) {
   const int cap = S.cap;
-  const int step = scan_step<R, LID>(cap);
-  const int rowb = cap * (int)sizeof(R4<R>);
   if (wave == 0) dma_copy(S.ray_tab, L.rayoff, (int)wave_tab_bytes<R>());
-  if (ne > 0) dma_copy(S.obst + (size_t)e0 * cap, L.row(0), min(step, ne) * rowb);
-  if (ne > step) dma_copy(S.obst + (size_t)(e0 + step) * cap, L.row(1), min(step, ne - step) * rowb);
+  if (ne > 0) dma_copy(S.obst + (size_t)e0 * cap, L.row0, min(scan_step<R, LID>(cap), ne) * cap * (int)sizeof(R4<R>));
 #pragma unroll
   for (int i = 0; i < 4; ++i) L.slot[i * 64 + lane_id()] = ~0ull;
 }
@@ -981,19 +978,17 @@ __device__ __forceinline__ void scan_envs(const State<R>& S, const IO<R>& io, co
       }
     }
   };
-  for (int k = 0, it = 0; k < ne; k += step, ++it) {
-    R4<R>* cur = L.row(it % kRowBufs);
+  for (int k = 0; k < ne; k += step) {
+    R4<R>* cur = ((k / step) & 1) ? L.row1 : L.row0;
     prof.mark(4);
-    // rows of iteration `it` landed.  Iterations 0 and 1 came with the prologue (waited for
-    // before the loop).  Later ones were issued at the top of iteration it-2, and the two
-    // sensor-row stores of every env of iterations it-2 and it-1 (full iterations: 4*step
-    // stores) were issued after them, so everything older than the last 4*step ops is done.
-    if (it >= 2) {
-      if (step == 2) vm_wait<8>(); else vm_wait<4>();
+    // rows of this iteration landed: every env of the previous iteration issued its two
+    // sensor-row stores after their DMA (a full pair: four), so all older ops are done
+    if (k > 0) {
+      if (step == 2) vm_wait<4>(); else vm_wait<2>();
     }
-    if (k + 2 * step < ne)
-      dma_copy(S.obst + (size_t)(e0 + k + 2 * step) * cap, L.row((it + 2) % kRowBufs),
-               min(step, ne - k - 2 * step) * rowb);
+    if (k + step < ne)
+      dma_copy(S.obst + (size_t)(e0 + k + step) * cap, ((k / step) & 1) ? L.row0 : L.row1,
+               min(step, ne - k - step) * rowb);
     prof.mark(1);
     prof.count(7);
     if constexpr (std::is_same<R, float>::value && (LID & kLidWindow) != 0) {
