@@ -879,8 +879,8 @@ template <typename R> __host__ __device__ constexpr size_t scan_rowbuf_bytes(int
 template <typename R> __host__ __device__ constexpr size_t lds_scan_slice(int cap) {
   return 256 * 8 + 64 * 4 + 2 * scan_rowbuf_bytes<R>(cap);
 }
-template <typename R> __host__ __device__ size_t lds_scan_bytes(int cap) {
-  return wave_tab_bytes<R>() + kWaves * lds_scan_slice<R>(cap);
+template <typename R> __host__ __device__ size_t lds_scan_bytes(int cap, int waves = kWaves) {
+  return wave_tab_bytes<R>() + waves * lds_scan_slice<R>(cap);
 }
 
 // LDS-DMA copy of `bytes` (multiple of 16, <= 2 KiB) from global `src` into the wave-uniform
@@ -1112,12 +1112,14 @@ __global__ __launch_bounds__(kBlock) void dyn_kernel(State<R> S, IO<R> io) {
   io.trunc[e] = trunc;
 }
 
-template <typename R, int MODE, int EPW, int LID>
+// WPB waves per block: 4 (256 threads) or 1 (64 threads: many small blocks, so the hardware
+// dispatcher refills a SIMD as soon as one wave finishes and the drain tail is one small block)
+template <typename R, int MODE, int EPW, int LID, int WPB>
 __device__ __forceinline__ void scan_body(const State<R>& S, const IO<R>& io) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);   // wave-uniform (SGPR)
+  const int wave = WPB == 1 ? 0 : __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);   // SGPR
   const int l = lane_id();
-  const int e0 = (blockIdx.x * kWaves + wave) * EPW;
+  const int e0 = (blockIdx.x * WPB + wave) * EPW;
   const int ne = min(EPW, S.N - e0);
   const ScanLds<R> L = scan_lds<R>(lds, wave, S.cap);
   Prof prof;
@@ -1139,17 +1141,17 @@ __device__ __forceinline__ void scan_body(const State<R>& S, const IO<R>& io) {
   USV_STAMP_W(3);
   scan_epilogue<R, MODE>(S, io, e0, ne, R(0), false, term_m, coll_m, trunc_m);
   prof.mark(5);
-  prof.flush(blockIdx.x * kWaves + wave);
+  prof.flush(blockIdx.x * WPB + wave);
   USV_STAMP_W(6);
 }
 
-template <typename R, int MODE, int EPW, int LID>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(80), amdgpu_num_vgpr(64)))
-void scan_kernel_tight(State<R> S, IO<R> io) { scan_body<R, MODE, EPW, LID>(S, io); }
+template <typename R, int MODE, int EPW, int LID, int WPB>
+__global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_num_sgpr(80), amdgpu_num_vgpr(64)))
+void scan_kernel_tight(State<R> S, IO<R> io) { scan_body<R, MODE, EPW, LID, WPB>(S, io); }
 
-template <typename R, int MODE, int EPW, int LID>
-__global__ __launch_bounds__(kBlock) void scan_kernel(State<R> S, IO<R> io) {
-  scan_body<R, MODE, EPW, LID>(S, io);
+template <typename R, int MODE, int EPW, int LID, int WPB>
+__global__ __launch_bounds__(kWave * WPB) void scan_kernel(State<R> S, IO<R> io) {
+  scan_body<R, MODE, EPW, LID, WPB>(S, io);
 }
 
 // 8 blocks of 256 threads per CU need <= 64 VGPRs and .sgpr_count <= 80 (MI355X_MICROARCH.md,
@@ -1528,23 +1530,23 @@ void* pick_wave(int epw, int lid, size_t* lds, int cap) {
   return pick_wave_lid<R, MODE, 8>(lid);
 }
 
-template <typename R, int MODE, int EPW>
+template <typename R, int MODE, int EPW, int WPB>
 void* pick_scan_lid(int lid) {
   if constexpr (std::is_same<R, float>::value && MODE == USV_MODE_SIMPLE) {
-    if (lid == 0) return (void*)&scan_kernel_tight<R, MODE, EPW, 0>;
-    if (lid == 3) return (void*)&scan_kernel_tight<R, MODE, EPW, 3>;
-    return (void*)&scan_kernel_tight<R, MODE, EPW, 7>;
+    if (lid == 0) return (void*)&scan_kernel_tight<R, MODE, EPW, 0, WPB>;
+    if (lid == 3) return (void*)&scan_kernel_tight<R, MODE, EPW, 3, WPB>;
+    return (void*)&scan_kernel_tight<R, MODE, EPW, 7, WPB>;
   }
-  if (lid == 0) return (void*)&scan_kernel<R, MODE, EPW, 0>;
-  if (lid == 3) return (void*)&scan_kernel<R, MODE, EPW, 3>;
-  return (void*)&scan_kernel<R, MODE, EPW, 7>;
+  if (lid == 0) return (void*)&scan_kernel<R, MODE, EPW, 0, WPB>;
+  if (lid == 3) return (void*)&scan_kernel<R, MODE, EPW, 3, WPB>;
+  return (void*)&scan_kernel<R, MODE, EPW, 7, WPB>;
 }
-template <typename R, int MODE>
+template <typename R, int MODE, int WPB>
 void* pick_scan(int epw, int lid) {
-  if (epw == 1) return pick_scan_lid<R, MODE, 1>(lid);
-  if (epw == 2) return pick_scan_lid<R, MODE, 2>(lid);
-  if (epw == 8) return pick_scan_lid<R, MODE, 8>(lid);
-  return pick_scan_lid<R, MODE, 4>(lid);
+  if (epw == 1) return pick_scan_lid<R, MODE, 1, WPB>(lid);
+  if (epw == 2) return pick_scan_lid<R, MODE, 2, WPB>(lid);
+  if (epw == 8) return pick_scan_lid<R, MODE, 8, WPB>(lid);
+  return pick_scan_lid<R, MODE, 4, WPB>(lid);
 }
 
 template <typename R>
@@ -1559,14 +1561,20 @@ int launch_step(Handle* h, State<R>& S, const float* act, float* obs, void* rew,
   const int epb = h->epb, lid = h->lid;
   void* fn;
   size_t lds;
-  if (h->kind == 2) {                                       // split: dynamics, then scan
+  if (h->kind == 2 || h->kind == 3) {                       // split: dynamics, then scan
     void* args[] = {(void*)&S, (void*)&io};
     void* dyn = h->cfg.mode == USV_MODE_SIMPLE ? (void*)&dyn_kernel<R, USV_MODE_SIMPLE>
                                                : (void*)&dyn_kernel<R, USV_MODE_ASMC_SIMPLE>;
     HIP_TRY(hipLaunchKernel(dyn, dim3((S.N + kBlock - 1) / kBlock), dim3(kBlock), args, 0, st));
-    fn = h->cfg.mode == USV_MODE_SIMPLE ? pick_scan<R, USV_MODE_SIMPLE>(epb / kWaves, lid)
-                                        : pick_scan<R, USV_MODE_ASMC_SIMPLE>(epb / kWaves, lid);
-    HIP_TRY(hipLaunchKernel(fn, dim3((S.N + epb - 1) / epb), dim3(kBlock), args, lds_scan_bytes<R>(S.cap), st));
+    if (h->kind == 2) {                                     // 4-wave blocks, epb envs each
+      fn = h->cfg.mode == USV_MODE_SIMPLE ? pick_scan<R, USV_MODE_SIMPLE, kWaves>(epb / kWaves, lid)
+                                          : pick_scan<R, USV_MODE_ASMC_SIMPLE, kWaves>(epb / kWaves, lid);
+      HIP_TRY(hipLaunchKernel(fn, dim3((S.N + epb - 1) / epb), dim3(kBlock), args, lds_scan_bytes<R>(S.cap), st));
+    } else {                                                // 1-wave blocks, epb envs each
+      fn = h->cfg.mode == USV_MODE_SIMPLE ? pick_scan<R, USV_MODE_SIMPLE, 1>(epb, lid)
+                                          : pick_scan<R, USV_MODE_ASMC_SIMPLE, 1>(epb, lid);
+      HIP_TRY(hipLaunchKernel(fn, dim3((S.N + epb - 1) / epb), dim3(kWave), args, lds_scan_bytes<R>(S.cap, 1), st));
+    }
     return USV_OK;
   }
   if (h->kind == 1) {
@@ -1780,7 +1788,9 @@ int usv_create(const usv_config* cfg, int32_t device, void** out) {
     const int got = std::sscanf(v, "%d,%d,%d", &epb, &lid, &kind);
     const bool blk_ok = kind == 0 && (epb == 16 || epb == 32 || epb == 64);
     const bool wave_ok = kind == 1 && (epb == 16 || epb == 32 || epb == 64) && (lid == 0 || lid == 3 || lid == 7);
-    const bool split_ok = kind == 2 && (epb == 4 || epb == 8 || epb == 16 || epb == 32) && (lid == 0 || lid == 3 || lid == 7);
+    const bool split_ok = ((kind == 2 && (epb == 4 || epb == 8 || epb == 16 || epb == 32)) ||
+                           (kind == 3 && (epb == 1 || epb == 2 || epb == 4 || epb == 8))) &&
+                          (lid == 0 || lid == 3 || lid == 7);
     if (got >= 2 && (blk_ok || wave_ok || split_ok) && lid >= 0 && lid <= 7) {
       h->epb = epb;
       h->lid = lid;
