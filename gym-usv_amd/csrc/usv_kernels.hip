@@ -660,8 +660,8 @@ __device__ __forceinline__ void lidar_window2(float dx, float dy, float key, flo
   B.rd1 = b1s != ~0ull ? __uint_as_float((unsigned)b1s) : (float)kSensorMax;
 }
 
-// rows: LDS, env A's row at [0, nA), env B's at [bofs, bofs + nB); nB = 0 when there is no env B.
-__device__ __forceinline__ void lidar_wave2(const float4* rows, int bofs, int nA, int nB, const Pose2& P,
+// rows: LDS, env A's row at [0, cap), env B's at [cap, 2 cap); nB = 0 when there is no env B.
+__device__ __forceinline__ void lidar_wave2(const float4* rows, int cap, int nA, int nB, const Pose2& P,
                                             const float2* rayoff, unsigned long long* slot, int* mark,
                                             Scan<float>& A, Scan<float>& B) {
   const int l = lane_id();
@@ -671,7 +671,7 @@ __device__ __forceinline__ void lidar_wave2(const float4* rows, int bofs, int nA
   const float px = hb ? P.pxB : P.pxA, py = hb ? P.pyB : P.pyA;
   const float sp = hb ? P.spB : P.spA, cp = hb ? P.cpB : P.cpA;
   float ox = 0.0f, oy = 0.0f, rr = 0.0f;
-  if (valid) { const float4 o = rows[(hb ? bofs : 0) + jl]; ox = o.x; oy = o.y; rr = o.z; }
+  if (valid) { const float4 o = rows[(hb ? cap : 0) + jl]; ox = o.x; oy = o.y; rr = o.z; }
   const float dx = ox - px, dy = oy - py;
   const float d = l_sqrt(m_fma(dx, dx, dy * dy));
   const float key = valid ? d - rr : big<float>();                              // simple_env.py:205-206
@@ -680,7 +680,7 @@ __device__ __forceinline__ void lidar_wave2(const float4* rows, int bofs, int nA
   A.far = B.far = false;
   const bool far = ballot(valid & (d >= (float)(0.99 * kSensorMax))) != 0;
   const WinLds W{slot, mark, rayoff};
-  const int boff = bofs - 32;                         // lane j >= 32 -> row index bofs + (j - 32)
+  const int boff = cap - 32;                          // lane j >= 32 -> row index cap + (j - 32)
   if (!far) lidar_window2<false>(dx, dy, key, d, rr, valid, sp, cp, P, rows, boff, W, A, B);
   else lidar_window2<true>(dx, dy, key, d, rr, valid, sp, cp, P, rows, boff, W, A, B);
 }
@@ -903,22 +903,6 @@ __device__ __forceinline__ void dma_copy(const void* src, void* dst, int bytes) 
     }
   }
 }
-// LDS-DMA of only the valid obstacles of a pair of envs: A's first nA rows, then B's first nB
-// rows packed right after them (per-lane source addresses, lane-linear LDS destination); f32
-// AoS rows (16 B per obstacle), nA + nB <= 64.
-__device__ __forceinline__ void dma_rows2(const void* srcA, int nA, const void* srcB, int nB, void* dst) {
-  const int c = lane_id();
-  const unsigned d = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)dst);
-  if (c < nA + nB) {
-    const char* g = c < nA ? reinterpret_cast<const char*>(srcA) + 16 * (size_t)c
-                           : reinterpret_cast<const char*>(srcB) + 16 * (size_t)(c - nA);
-    unsigned keep;
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-                 "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(g), "s"(d) : "memory");
-  }
-}
-
 // Wait until at most N vector-memory operations are outstanding (gfx9 vmcnt counts loads,
 // LDS-DMA and stores in issue order): everything older than the last N has completed.
 template <int N> __device__ __forceinline__ void vm_wait() {
@@ -1002,17 +986,9 @@ __device__ __forceinline__ void scan_envs(const State<R>& S, const IO<R>& io, co
     if (k > 0) {
       if (step == 2) vm_wait<4>(); else vm_wait<2>();
     }
-    if (k + step < ne) {
-      R4<R>* nxt = ((k / step) & 1) ? L.row0 : L.row1;
-      const int kn = k + step;
-      if (step == 2) {                                   // valid obstacles only, B packed after A
-        const int nA = __builtin_amdgcn_readlane(nl, kn);
-        const int nB = kn + 1 < ne ? __builtin_amdgcn_readlane(nl, kn + 1) : 0;
-        dma_rows2(S.obst + (size_t)(e0 + kn) * cap, nA, S.obst + (size_t)(e0 + kn + 1) * cap, nB, nxt);
-      } else {
-        dma_copy(S.obst + (size_t)(e0 + kn) * cap, nxt, min(step, ne - kn) * rowb);
-      }
-    }
+    if (k + step < ne)
+      dma_copy(S.obst + (size_t)(e0 + k + step) * cap, ((k / step) & 1) ? L.row0 : L.row1,
+               min(step, ne - k - step) * rowb);
     prof.mark(1);
     prof.count(7);
     if constexpr (std::is_same<R, float>::value && (LID & kLidWindow) != 0) {
@@ -1022,9 +998,7 @@ __device__ __forceinline__ void scan_envs(const State<R>& S, const IO<R>& io, co
         const Pose2 PP{bcast(P.x, k), bcast(P.y, k), bcast(P.z, k), bcast(P.w, k),
                        bcast(P.x, kb), bcast(P.y, kb), bcast(P.z, kb), bcast(P.w, kb)};
         Scan<float> sa, sb;
-        // iteration 0 came with the prologue as whole rows (B at cap); later ones valid-only
-        const int nA = __builtin_amdgcn_readlane(nl, k);
-        lidar_wave2(reinterpret_cast<const float4*>(cur), k == 0 ? cap : nA, nA,
+        lidar_wave2(reinterpret_cast<const float4*>(cur), cap, __builtin_amdgcn_readlane(nl, k),
                     hasB ? __builtin_amdgcn_readlane(nl, kb) : 0, PP, L.rayoff, L.slot, L.mark, sa, sb);
         prof.mark(2);
         emit(k, sa);
