@@ -960,8 +960,12 @@ __device__ __forceinline__ void scan_envs(const State<R>& S, const IO<R>& io, co
     coll_m |= (unsigned)coll << k;
     const float s0 = (float)l_norm(sc.rd0), s1 = (float)l_norm(sc.rd1);        // :82-83
     float* row = io.obs + (size_t)e * kObsDim;
+#ifdef USV_ABL_NOSTORE   // diagnostic ablation only: sensor half of the obs row not written
+    if (s0 == 12345.0f) row[kHdr + l] = s1;
+#else
     row[kHdr + l] = s0;                                        // stale scan is kept by reset
     row[kHdr + 64 + l] = s1;
+#endif
     if (done) {
       if (io.fobs) {                                           // terminal obs
         float* f = io.fobs + (size_t)e * kObsDim;
@@ -998,8 +1002,13 @@ __device__ __forceinline__ void scan_envs(const State<R>& S, const IO<R>& io, co
         const Pose2 PP{bcast(P.x, k), bcast(P.y, k), bcast(P.z, k), bcast(P.w, k),
                        bcast(P.x, kb), bcast(P.y, kb), bcast(P.z, kb), bcast(P.w, kb)};
         Scan<float> sa, sb;
+#ifdef USV_ABL_NOLIDAR   // diagnostic ablation only: readings from the row, no scan
+        sa.rd0 = sb.rd0 = reinterpret_cast<const float4*>(cur)[lane_id() & 31].x + PP.pxA;
+        sa.rd1 = sb.rd1 = PP.pyB; sa.term = sb.term = false; sa.far = sb.far = false;
+#else
         lidar_wave2(reinterpret_cast<const float4*>(cur), cap, __builtin_amdgcn_readlane(nl, k),
                     hasB ? __builtin_amdgcn_readlane(nl, kb) : 0, PP, L.rayoff, L.slot, L.mark, sa, sb);
+#endif
         prof.mark(2);
         emit(k, sa);
         if (hasB) emit(k + 1, sb);
@@ -1060,7 +1069,12 @@ __device__ __forceinline__ void step_body_wave(const State<R>& S, const IO<R>& i
     const int e = e0 + min(l, ne - 1);
     const float2 a = reinterpret_cast<const float2*>(io.act)[e];
     float hdr[kHdr];
+#ifdef USV_ABL_NODYN     // diagnostic ablation only: pose from x, y, action; no dynamics
+    px = S.F(F_X)[e]; py = S.F(F_Y)[e]; sp = R(a.x); cp = R(a.y); partial = R(0); trunc = false;
+    for (int i = 0; i < kHdr; ++i) hdr[i] = (float)px;
+#else
     env_dynamics<R, MODE>(S, e, a.x, a.y, hdr, px, py, sp, cp, partial, trunc);
+#endif
     float* row = io.obs + (size_t)e * kObsDim;
 #pragma unroll
     for (int i = 0; i < kHdr; ++i) row[i] = hdr[i];
