@@ -50,8 +50,10 @@ template <typename R> struct State {
   R* asmc;                 // [16][N]
   R* v0;                   // [19][fstride] usv-asmc-v0: last[9], aux[3], target[6], action_last
   const R* ray_tab;        // [128][2] (cos, sin)(start + i*res)
-  R4<R>* pose;             // [N] (x, y, sin psi, cos psi) after the step's dynamics (split step)
+  R4<R>* pose;             // [N][2] pose record after the step's dynamics (split step):
+                           //   (x, y, sin psi, cos psi), (partial reward, n_obs, truncated, 0)
   int N, cap, limit, autoreset;
+  int prio;                // scan loops: raise the issue priority of lagging waves (s_setprio)
   int fstride;             // elements between fields (>= N, 256-B aligned)
   uint64_t seed, gid0;
   __host__ __device__ R* F(int i) const { return freal + (size_t)i * fstride; }
@@ -87,13 +89,31 @@ __device__ unsigned long long g_stamps[32768 * kStampSlots];
     if (threadIdx.x == 0 && blockIdx.x < 32768)                                           \
       g_stamps[blockIdx.x * kStampSlots + (i)] = __builtin_amdgcn_s_memrealtime();        \
   } while (0)
-#define USV_STAMP_W(i)                                                                    \
+// block slot, written by the first lane of whichever wave executes it (kind 0)
+#define USV_STAMP_B(i)                                                                    \
   do {                                                                                    \
     if ((threadIdx.x & 63) == 0 && blockIdx.x < 32768)                                    \
       g_stamps[blockIdx.x * kStampSlots + (i)] = __builtin_amdgcn_s_memrealtime();        \
   } while (0)
+// wave slot (global wave index; kinds 1-3)
+#define USV_STAMP_W(i)                                                                    \
+  do {                                                                                    \
+    const unsigned gw_ = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;               \
+    if ((threadIdx.x & 63) == 0 && gw_ < 32768)                                           \
+      g_stamps[gw_ * kStampSlots + (i)] = __builtin_amdgcn_s_memrealtime();               \
+  } while (0)
+// slot 7: HW_ID (SIMD, CU, SE bits) | XCC_ID << 32 of the wave
+#define USV_STAMP_ID()                                                                    \
+  do {                                                                                    \
+    const unsigned gw_ = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;               \
+    const unsigned long long hw_ = __builtin_amdgcn_s_getreg((31 << 11) | 4);             \
+    const unsigned long long xcc_ = __builtin_amdgcn_s_getreg((15 << 11) | 20);           \
+    if ((threadIdx.x & 63) == 0 && gw_ < 32768) g_stamps[gw_ * kStampSlots + 7] = hw_ | (xcc_ << 32); \
+  } while (0)
 #else
+#define USV_STAMP_ID() do {} while (0)
 #define USV_STAMP(i) do {} while (0)
+#define USV_STAMP_B(i) do {} while (0)
 #define USV_STAMP_W(i) do {} while (0)
 #endif
 // Diagnostic build only (-DUSV_DIAG_PROF): per-wave shader-clock (s_memtime) cycles spent in
@@ -340,9 +360,16 @@ template <> __device__ __forceinline__ float l_sqrt(float x) { return __builtin_
 template <typename R> __device__ __forceinline__ R l_norm(R x) { return x / R(kSensorMax); }
 template <> __device__ __forceinline__ float l_norm(float x) { return x * 0.01f; }
 
-// ray direction = rotation of the ray-offset table entry (start + i*res) by the heading
+// Ray frame.  Obstacles are rotated once into the frame of ray 0 (heading - 120 deg): a along
+// ray 0, b to its left; ray i is then (cos i*res, sin i*res) from the table, and for every
+// (ray, obstacle) pair proj = a cos + b sin, perp = a sin - b cos -- the reference's projection
+// (usv_asmc_ca_env.py:506-518) with both vectors in that frame, so no per-pair rotation.
 template <typename R> __device__ __forceinline__ R ray_c(R cp, R sp, R co, R so) { return m_fma(cp, co, -(sp * so)); }
 template <typename R> __device__ __forceinline__ R ray_s(R cp, R sp, R co, R so) { return m_fma(sp, co, cp * so); }
+template <typename R> __device__ __forceinline__ void to_ray0(R dx, R dy, R c0, R s0, R& a, R& b) {
+  a = m_fma(dx, c0, dy * s0);
+  b = m_fma(dy, c0, -(dx * s0));
+}
 
 template <typename R, bool RANGE_CHECK>
 __device__ __forceinline__ void ray_pair(Ray<R>& ra, R jdx, R jdy, R jr2, R jk, int j) {
@@ -441,6 +468,8 @@ __device__ __forceinline__ void lidar_brute(R dx, R dy, R r2, R key, R d, R rr, 
                                             Scan<R>& out) {
   const int l = lane_id();
   int m = n;
+  R a, b;
+  to_ray0(dx, dy, ray_c(cp, sp, R(kStartC), R(kStartS)), ray_s(cp, sp, R(kStartC), R(kStartS)), a, b);
   if (LID & kLidSkip) {
     const R wx = cp * R(kBlindC) - sp * R(kBlindS), wy = sp * R(kBlindC) + cp * R(kBlindS);
     const R dot = dx * wx + dy * wy;
@@ -453,8 +482,8 @@ __device__ __forceinline__ void lidar_brute(R dx, R dy, R r2, R key, R d, R rr, 
     m = __popcll(ball);
     const int pos = __builtin_amdgcn_mbcnt_hi((unsigned)(ball >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)ball, 0));
     const int dst = keep ? pos : 63;               // dropped lanes all land in lane 63 (unused)
-    dx = __builtin_bit_cast(R, permute(dst, __builtin_bit_cast(typename Bits<R>::T, dx)));
-    dy = __builtin_bit_cast(R, permute(dst, __builtin_bit_cast(typename Bits<R>::T, dy)));
+    a = __builtin_bit_cast(R, permute(dst, __builtin_bit_cast(typename Bits<R>::T, a)));
+    b = __builtin_bit_cast(R, permute(dst, __builtin_bit_cast(typename Bits<R>::T, b)));
     r2 = __builtin_bit_cast(R, permute(dst, __builtin_bit_cast(typename Bits<R>::T, r2)));
     key = __builtin_bit_cast(R, permute(dst, __builtin_bit_cast(typename Bits<R>::T, key)));
   }
@@ -462,12 +491,12 @@ __device__ __forceinline__ void lidar_brute(R dx, R dy, R r2, R key, R d, R rr, 
     if (l >= m) { r2 = R(-1); key = big<R>(); }    // padding obstacle: delta < 0, never hit
     m = (m + 1) & ~1;
   }
-  Ray<R> r0{ray_c(cp, sp, co0, so0), ray_s(cp, sp, co0, so0), big<R>(), -1};
-  Ray<R> r1{ray_c(cp, sp, co1, so1), ray_s(cp, sp, co1, so1), big<R>(), -1};
-  if (!far) ray_loop<R, false, (LID & kLidUnroll2) != 0>(r0, r1, dx, dy, r2, key, m);
-  else ray_loop<R, true, (LID & kLidUnroll2) != 0>(r0, r1, dx, dy, r2, key, m);
-  out.rd0 = reading_of(r0.c, r0.s, r0.bj, dx, dy, r2);
-  out.rd1 = reading_of(r1.c, r1.s, r1.bj, dx, dy, r2);
+  Ray<R> r0{co0, so0, big<R>(), -1};
+  Ray<R> r1{co1, so1, big<R>(), -1};
+  if (!far) ray_loop<R, false, (LID & kLidUnroll2) != 0>(r0, r1, a, b, r2, key, m);
+  else ray_loop<R, true, (LID & kLidUnroll2) != 0>(r0, r1, a, b, r2, key, m);
+  out.rd0 = reading_of(r0.c, r0.s, r0.bj, a, b, r2);
+  out.rd1 = reading_of(r1.c, r1.s, r1.bj, a, b, r2);
 }
 
 // Angular-window lidar (f32).  Lane j computes the ray-index windows its obstacle can touch
@@ -518,7 +547,8 @@ __device__ __forceinline__ void lidar_window(float dx, float dy, float key, floa
   const int l = lane_id();
   const float c0r = ray_c(cp, sp, (float)kStartC, (float)kStartS);
   const float s0r = ray_s(cp, sp, (float)kStartC, (float)kStartS);
-  const float a = dx * c0r + dy * s0r, b = dy * c0r - dx * s0r;
+  float a, b;
+  to_ray0(dx, dy, c0r, s0r, a, b);
   const float phi = fast_atan2(b, a);                 // CCW angle from ray 0; ray i at i*res
   // |err| of the window edges: fast_atan2 < 2e-5 rad, float rounding ~1e-6 rad; a ray
   // 1e-5 rad outside the true extent already fails the exact test by ~r*d*1e-5 >> ulp
@@ -561,13 +591,12 @@ __device__ __forceinline__ void lidar_window(float dx, float dy, float key, floa
     const unsigned gk = (unsigned)__shfl((int)ok, jj, kWave);
     const int l1 = mj & 255, n1 = (mj >> 8) & 255, l2 = mj >> 16;
     const int i = min(max((k < n1 ? l1 : l2 - n1) + k, 0), 127);
-    float gx, gy, gr;
+    float gx, gy, gr, ga, gb;
     row.get(jj, gx, gy, gr);
-    const float gdx = gx - px, gdy = gy - py;
+    to_ray0(gx - px, gy - py, c0r, s0r, ga, gb);
     const float2 cs = L.rayoff[i];
-    const float c = ray_c(cp, sp, cs.x, cs.y), s = ray_s(cp, sp, cs.x, cs.y);
-    const float proj = fmaf(gdx, c, gdy * s);
-    const float perp = fmaf(gdx, s, -(gdy * c));
+    const float proj = fmaf(ga, cs.x, gb * cs.y);
+    const float perp = fmaf(ga, cs.y, -(gb * cs.x));
     const float delta = fmaf(-perp, perp, gr * gr);
     const float dist = proj - l_sqrt(delta);                 // reading if this pair wins (:457)
     bool hit = (q < W) & (proj >= 0.0f) & (delta >= 0.0f);
@@ -591,14 +620,18 @@ __device__ __forceinline__ void lidar_window(float dx, float dy, float key, floa
 // readings are bit-identical to one-env-per-wave.  Slots [256]: env A rays, then env B rays.
 struct Pose2 { float pxA, pyA, spA, cpA, pxB, pyB, spB, cpB; };    // wave-uniform
 
+// The obstacle lanes leave (a, b, r^2, key bits) records in the rows buffer (lane j at slot j;
+// each lane overwrites only what one ds instruction of this wave has already read), and each
+// pair reads its owner's record: no pose select, no rotation and no re-read of the row per pair.
 template <bool RANGE_CHECK>
 __device__ __forceinline__ void lidar_window2(float dx, float dy, float key, float d, float rr, bool valid,
-                                              float sp, float cp, const Pose2& P, const float4* rows,
-                                              int boff, const WinLds& L, Scan<float>& A, Scan<float>& B) {
+                                              float sp, float cp, float4* rec, const WinLds& L,
+                                              Scan<float>& A, Scan<float>& B) {
   const int l = lane_id();
   const float c0r = ray_c(cp, sp, (float)kStartC, (float)kStartS);
   const float s0r = ray_s(cp, sp, (float)kStartC, (float)kStartS);
-  const float a = dx * c0r + dy * s0r, b = dy * c0r - dx * s0r;
+  float a, b;
+  to_ray0(dx, dy, c0r, s0r, a, b);
   const float phi = fast_atan2(b, a);                 // CCW angle from ray 0; ray i at i*res
   const float margin = (float)(0.25 * kRes);          // see lidar_window
   const bool inside = d <= rr * 1.001f;
@@ -616,12 +649,12 @@ __device__ __forceinline__ void lidar_window2(float dx, float dy, float key, flo
   const int off = incl - cnt;
   const int W = __builtin_amdgcn_readlane(incl, 63);
   const int meta = lo1 | (len1 << 8) | (lo2 << 16);
-  const unsigned ok = ord_key(key);
+  rec[l] = make_float4(a, b, rr * rr, __uint_as_float(ord_key(key)));
   int carry = 0;                                      // owner marks are lane + 1; 0 = none
   for (int base = 0; base < W; base += kWave) {       // wave-uniform pass count
     L.mark[l] = 0;
     if (cnt > 0 && off >= base && off < base + kWave) L.mark[off - base] = l + 1;
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");   // marks and records visible
     __builtin_amdgcn_wave_barrier();
     const int j1 = max(wave_incl_max(L.mark[l]), carry);
     carry = __builtin_amdgcn_readlane(j1, 63);
@@ -629,24 +662,18 @@ __device__ __forceinline__ void lidar_window2(float dx, float dy, float key, flo
     const int q = base + l;
     const int k = q - __shfl(off, jj, kWave);
     const int mj = __shfl(meta, jj, kWave);
-    const unsigned gk = (unsigned)__shfl((int)ok, jj, kWave);
     const int l1 = mj & 255, n1 = (mj >> 8) & 255, l2 = mj >> 16;
     const int i = min(max((k < n1 ? l1 : l2 - n1) + k, 0), 127);
-    const bool ob = jj >= 32;                         // owner's env
-    const float opx = ob ? P.pxB : P.pxA, opy = ob ? P.pyB : P.pyA;
-    const float osp = ob ? P.spB : P.spA, ocp = ob ? P.cpB : P.cpA;
-    const float4 o = rows[jj + (ob ? boff : 0)];
-    const float gdx = o.x - opx, gdy = o.y - opy, gr = o.z;
+    const float4 o = rec[jj];                         // owner's (a, b, r^2, key bits)
     const float2 cs = L.rayoff[i];
-    const float c = ray_c(ocp, osp, cs.x, cs.y), s = ray_s(ocp, osp, cs.x, cs.y);
-    const float proj = fmaf(gdx, c, gdy * s);
-    const float perp = fmaf(gdx, s, -(gdy * c));
-    const float delta = fmaf(-perp, perp, gr * gr);
+    const float proj = fmaf(o.x, cs.x, o.y * cs.y);
+    const float perp = fmaf(o.x, cs.y, -(o.y * cs.x));
+    const float delta = fmaf(-perp, perp, o.z);
     const float dist = proj - l_sqrt(delta);
     bool hit = (q < W) & (proj >= 0.0f) & (delta >= 0.0f);
     if (RANGE_CHECK) hit = hit && dist < (float)kSensorMax;   // :458
-    if (hit)
-      atomicMin(&L.slot[(ob ? 128 : 0) + i], ((unsigned long long)gk << 32) | __float_as_uint(dist));
+    if (hit)                                          // slots: env A's rays, then env B's
+      atomicMin(&L.slot[(jj >= 32 ? 128 : 0) + i], ((unsigned long long)__float_as_uint(o.w) << 32) | __float_as_uint(dist));
   }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");     // all lanes' ds_min_u64 landed
   __builtin_amdgcn_wave_barrier();
@@ -661,7 +688,7 @@ __device__ __forceinline__ void lidar_window2(float dx, float dy, float key, flo
 }
 
 // rows: LDS, env A's row at [0, cap), env B's at [cap, 2 cap); nB = 0 when there is no env B.
-__device__ __forceinline__ void lidar_wave2(const float4* rows, int cap, int nA, int nB, const Pose2& P,
+__device__ __forceinline__ void lidar_wave2(float4* rows, int cap, int nA, int nB, const Pose2& P,
                                             const float2* rayoff, unsigned long long* slot, int* mark,
                                             Scan<float>& A, Scan<float>& B) {
   const int l = lane_id();
@@ -680,9 +707,8 @@ __device__ __forceinline__ void lidar_wave2(const float4* rows, int cap, int nA,
   A.far = B.far = false;
   const bool far = ballot(valid & (d >= (float)(0.99 * kSensorMax))) != 0;
   const WinLds W{slot, mark, rayoff};
-  const int boff = cap - 32;                          // lane j >= 32 -> row index cap + (j - 32)
-  if (!far) lidar_window2<false>(dx, dy, key, d, rr, valid, sp, cp, P, rows, boff, W, A, B);
-  else lidar_window2<true>(dx, dy, key, d, rr, valid, sp, cp, P, rows, boff, W, A, B);
+  if (!far) lidar_window2<false>(dx, dy, key, d, rr, valid, sp, cp, rows, W, A, B);
+  else lidar_window2<true>(dx, dy, key, d, rr, valid, sp, cp, rows, W, A, B);
 }
 
 template <typename R, int LID, typename Row>
@@ -783,7 +809,7 @@ __device__ __forceinline__ void step_body(const State<R>& S, const IO<R>& io) {
       sh.trunc[l] = trunc;
       sh.n[l] = S.I(I_NOBS)[e];
     }
-    USV_STAMP_W(1);
+    USV_STAMP_B(1);
   } else {
     // ---- phase 1 (the other three waves): stage this block's obstacle rows in LDS (SoA)
     // meanwhile; staging wave sw = 0..2 takes rows sw, sw+3, ...; four loads in flight
@@ -939,6 +965,52 @@ __device__ __forceinline__ void scan_prologue(const State<R>& S, const ScanLds<R
   for (int i = 0; i < 4; ++i) L.slot[i * 64 + lane_id()] = ~0ull;
 }
 
+// VALU issue is arbitrated by priority, then age (MI355X_MICROARCH.md, Two waves per SIMD): with
+// a static split the oldest waves of a SIMD finish first and the youngest run alone at the end.
+// The scan loops lower a wave's priority as it progresses (3 at the start, 0 in its last
+// quarter), so the waves of a SIMD advance together and finish together.
+__device__ __forceinline__ void set_prio(int p) {   // p wave-uniform
+  if (p >= 3) __builtin_amdgcn_s_setprio(3);
+  else if (p == 2) __builtin_amdgcn_s_setprio(2);
+  else if (p == 1) __builtin_amdgcn_s_setprio(1);
+  else __builtin_amdgcn_s_setprio(0);
+}
+
+// Outputs of one scanned env e (wave-wide, lane l holds rays l and l + 64): the sensor half of
+// its obs row; for a done env the terminal obs and the stale scan; term / collision bit k.
+template <typename R, int MODE>
+__device__ __forceinline__ void emit_env(const State<R>& S, const IO<R>& io, int e, const Scan<R>& sc,
+                                         unsigned trunc_bit, int k, unsigned& term_m, unsigned& coll_m) {
+  const int l = lane_id();
+  const bool done = sc.term || trunc_bit;
+  const bool coll = ballot((sc.rd0 < R(kCollDist)) | (sc.rd1 < R(kCollDist))) != 0;  // :153-156
+  term_m |= (unsigned)sc.term << k;
+  coll_m |= (unsigned)coll << k;
+  const float s0 = (float)l_norm(sc.rd0), s1 = (float)l_norm(sc.rd1);        // :82-83
+  float* row = io.obs + (size_t)e * kObsDim;
+#ifdef USV_ABL_NOSTORE   // diagnostic ablation only: sensor half of the obs row not written
+  if (s0 == 12345.0f) row[kHdr + l] = s1;
+#else
+  row[kHdr + l] = s0;                                          // stale scan is kept by reset
+  row[kHdr + 64 + l] = s1;
+#endif
+  if (done) {
+    if (io.fobs) {                                             // terminal obs
+      float* f = io.fobs + (size_t)e * kObsDim;
+      f[kHdr + l] = s0;
+      f[kHdr + 64 + l] = s1;
+      // header: written earlier by this wave (wave kernel) or by dyn_kernel; a wavefront's
+      // own earlier stores are visible to its later loads
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      if (l < kHdr) f[l] = row[l];
+    }
+    if (S.autoreset == USV_AUTORESET_SAME_STEP) {
+      S.sensor_last[(size_t)e * kSensors + l] = sc.rd0;
+      S.sensor_last[(size_t)e * kSensors + 64 + l] = sc.rd1;
+    }
+  }
+}
+
 // The scan loop over this wave's ne envs.  Inputs lane-per-env (lane k = env e0 + k): pose
 // P = (x, y, sin psi, cos psi), obstacle count nl, truncation bits trunc_m.  Writes the sensor
 // half of each obs row, final obs and stale scan of done envs; returns term / collision bits.
@@ -947,43 +1019,17 @@ template <typename R, int MODE, int LID>
 __device__ __forceinline__ void scan_envs(const State<R>& S, const IO<R>& io, const ScanLds<R>& L, int e0,
                                           int ne, const R4<R>& P, int nl, unsigned trunc_m,
                                           unsigned& term_m, unsigned& coll_m, Prof& prof) {
-  const int l = lane_id();
   const int cap = S.cap;
   const int rowb = cap * (int)sizeof(R4<R>);
   const int step = scan_step<R, LID>(cap);
   term_m = 0; coll_m = 0;
   auto emit = [&](int k, const Scan<R>& sc) {               // outputs of env e0 + k
-    const int e = e0 + k;
-    const bool done = sc.term || ((trunc_m >> k) & 1);
-    const bool coll = ballot((sc.rd0 < R(kCollDist)) | (sc.rd1 < R(kCollDist))) != 0;  // :153-156
-    term_m |= (unsigned)sc.term << k;
-    coll_m |= (unsigned)coll << k;
-    const float s0 = (float)l_norm(sc.rd0), s1 = (float)l_norm(sc.rd1);        // :82-83
-    float* row = io.obs + (size_t)e * kObsDim;
-#ifdef USV_ABL_NOSTORE   // diagnostic ablation only: sensor half of the obs row not written
-    if (s0 == 12345.0f) row[kHdr + l] = s1;
-#else
-    row[kHdr + l] = s0;                                        // stale scan is kept by reset
-    row[kHdr + 64 + l] = s1;
-#endif
-    if (done) {
-      if (io.fobs) {                                           // terminal obs
-        float* f = io.fobs + (size_t)e * kObsDim;
-        f[kHdr + l] = s0;
-        f[kHdr + 64 + l] = s1;
-        // header: written earlier by this wave (wave kernel) or by dyn_kernel; a wavefront's
-        // own earlier stores are visible to its later loads
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (l < kHdr) f[l] = row[l];
-      }
-      if (S.autoreset == USV_AUTORESET_SAME_STEP) {
-        S.sensor_last[(size_t)e * kSensors + l] = sc.rd0;
-        S.sensor_last[(size_t)e * kSensors + 64 + l] = sc.rd1;
-      }
-    }
+    emit_env<R, MODE>(S, io, e0 + k, sc, (trunc_m >> k) & 1, k, term_m, coll_m);
   };
+  const int iters = (ne + step - 1) / step;
   for (int k = 0; k < ne; k += step) {
     R4<R>* cur = ((k / step) & 1) ? L.row1 : L.row0;
+    if (S.prio) set_prio(3 - (4 * (k / step)) / iters);
     prof.mark(4);
     // rows of this iteration landed: every env of the previous iteration issued its two
     // sensor-row stores after their DMA (a full pair: four), so all older ops are done
@@ -1006,7 +1052,7 @@ __device__ __forceinline__ void scan_envs(const State<R>& S, const IO<R>& io, co
         sa.rd0 = sb.rd0 = reinterpret_cast<const float4*>(cur)[lane_id() & 31].x + PP.pxA;
         sa.rd1 = sb.rd1 = PP.pyB; sa.term = sb.term = false; sa.far = sb.far = false;
 #else
-        lidar_wave2(reinterpret_cast<const float4*>(cur), cap, __builtin_amdgcn_readlane(nl, k),
+        lidar_wave2(reinterpret_cast<float4*>(cur), cap, __builtin_amdgcn_readlane(nl, k),
                     hasB ? __builtin_amdgcn_readlane(nl, kb) : 0, PP, L.rayoff, L.slot, L.mark, sa, sb);
 #endif
         prof.mark(2);
@@ -1057,6 +1103,8 @@ __device__ __forceinline__ void step_body_wave(const State<R>& S, const IO<R>& i
   const ScanLds<R> L = scan_lds<R>(lds, wave, S.cap);
   Prof prof;
   USV_STAMP_W(0);
+  USV_STAMP_ID();
+  if (S.prio) __builtin_amdgcn_s_setprio(3);
   scan_prologue<R, LID>(S, L, wave, e0, ne);
   // dynamics: lanes 0..ne-1; lanes >= ne recompute env ne-1 and store identical values to the
   // identical addresses (benign) -- no divergent memory operations, so hipcc's own vmcnt
@@ -1121,7 +1169,8 @@ __global__ __launch_bounds__(kBlock) void dyn_kernel(State<R> S, IO<R> io) {
   float* row = io.obs + (size_t)e * kObsDim;
 #pragma unroll
   for (int i = 0; i < kHdr; ++i) row[i] = hdr[i];
-  S.pose[e] = R4<R>{px, py, sp, cp};
+  S.pose[2 * (size_t)e] = R4<R>{px, py, sp, cp};
+  S.pose[2 * (size_t)e + 1] = R4<R>{partial, R(S.I(I_NOBS)[e]), R(trunc ? 1 : 0), R(0)};
   io.rew[e] = partial;
   io.trunc[e] = trunc;
 }
@@ -1138,11 +1187,12 @@ __device__ __forceinline__ void scan_body(const State<R>& S, const IO<R>& io) {
   const ScanLds<R> L = scan_lds<R>(lds, wave, S.cap);
   Prof prof;
   USV_STAMP_W(0);
+  USV_STAMP_ID();
   scan_prologue<R, LID>(S, L, wave, e0, ne);
   // per-env inputs, lane-per-env (lanes >= ne repeat env ne-1), read once: the scan loop then
   // issues no vector loads and its counted vm_wait stays exact
   const int ec = max(0, min(e0 + min(l, ne - 1), S.N - 1));
-  const R4<R> P = S.pose[ec];
+  const R4<R> P = S.pose[2 * (size_t)ec];
   const int nl = S.I(I_NOBS)[ec];
   const unsigned trunc_m = (unsigned)ballot(io.trunc[ec] != 0);
   vm_wait<0>();
@@ -1167,6 +1217,133 @@ template <typename R, int MODE, int EPW, int LID, int WPB>
 __global__ __launch_bounds__(kWave * WPB) void scan_kernel(State<R> S, IO<R> io) {
   scan_body<R, MODE, EPW, LID, WPB>(S, io);
 }
+
+// ---- block-queue step (f32 window lidar, cap <= 32): 1024-thread blocks of 16 waves own
+// kQEnvs envs each; the block's env pairs are pulled from an LDS counter.  VALU issue on a SIMD
+// is arbitrated by priority, then age, so with a static split the oldest waves finish first
+// and the youngest run alone at the end; with the queue the favoured waves simply take more
+// pairs and all of them finish together.  The block's queue position also sets every wave's
+// priority (lagging blocks first), which evens out the two blocks that share each SIMD.
+//   kind 5 (fused): waves 0 and 1 run the block's dynamics lane-per-env (full width) and leave
+//                   the pose records in LDS;
+//   kind 4 (split): dyn_kernel ran first and left them in S.pose; they are DMA'd into LDS.
+// Each wave's first pair is static (pair = wave); its rows and the next pair's are DMA'd while
+// the current pair is scanned.
+constexpr int kQWaves = 16, kQBlock = kQWaves * kWave, kQEnvs = 128;
+__host__ __device__ constexpr size_t lds_q_bytes(int cap) {
+  return wave_tab_bytes<float>() + kQWaves * lds_scan_slice<float>(cap) + kQEnvs * 2 * 16 + 16;
+}
+
+template <int MODE, bool FUSED>
+__device__ __forceinline__ void step_q_body(const State<float>& S, const IO<float>& io) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
+  const int l = lane_id();
+  const int cap = S.cap, rowb = cap * (int)sizeof(float4);
+  const int eb = blockIdx.x * kQEnvs;                  // this block's envs: eb .. eb + nbe - 1
+  const int nbe = min(kQEnvs, S.N - eb);
+  const int np = (nbe + 1) >> 1;                       // and pairs 0 .. np - 1 (block-local)
+  const ScanLds<float> L = scan_lds<float>(lds, wave, cap);
+  R4<float>* const rec = reinterpret_cast<R4<float>*>(lds + wave_tab_bytes<float>() + kQWaves * lds_scan_slice<float>(cap));
+  unsigned* const qctr = reinterpret_cast<unsigned*>(rec + 2 * kQEnvs);
+  if (threadIdx.x == 0) *qctr = kQWaves;                // pairs 0 .. kQWaves-1 are the static first ones
+  if (wave == 0) dma_copy(S.ray_tab, L.rayoff, (int)wave_tab_bytes<float>());
+#pragma unroll
+  for (int i = 0; i < 4; ++i) L.slot[i * 64 + l] = ~0ull;
+  USV_STAMP_W(0);
+  USV_STAMP_ID();
+  int cur = wave;
+  if (cur < np) dma_copy(S.obst + (size_t)(eb + 2 * cur) * cap, L.row0, min(2, nbe - 2 * cur) * rowb);
+  if constexpr (FUSED) {
+    if (wave < kQEnvs / kWave) {                        // phase 1: dynamics, one lane per env
+      const int k = min(wave * kWave + l, nbe - 1);     // lanes past the end repeat the last env
+      const int e = eb + k;
+      const float2 a = reinterpret_cast<const float2*>(io.act)[e];
+      float hdr[kHdr];
+      float px, py, sp, cp, partial;
+      bool trunc;
+      env_dynamics<float, MODE>(S, e, a.x, a.y, hdr, px, py, sp, cp, partial, trunc);
+      float* row = io.obs + (size_t)e * kObsDim;
+#pragma unroll
+      for (int i = 0; i < kHdr; ++i) row[i] = hdr[i];
+      io.trunc[e] = trunc;
+      rec[2 * k] = R4<float>{px, py, sp, cp};
+      rec[2 * k + 1] = R4<float>{partial, (float)S.I(I_NOBS)[e], trunc ? 1.0f : 0.0f, 0.0f};
+    }
+  } else {
+    static_assert(kQEnvs == 2 * kWave, "waves 0 and 1 copy 64 records (2 KiB) each");
+    if (wave < 2 && wave * kWave < nbe)
+      dma_copy(S.pose + 2 * (size_t)(eb + wave * kWave), rec + 2 * wave * kWave, min(kWave, nbe - wave * kWave) * 32);
+  }
+  // rows, ray table and records landed; the dynamics' header stores are complete before the
+  // barrier, so a done env's terminal obs can copy its header from the obs row
+  USV_STAMP_W(1);
+  vm_wait<0>();
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  USV_STAMP_W(2);
+  unsigned tk = 0;
+  if (l == 0) tk = atomicAdd(qctr, 1u);                 // LDS ticket of this wave's second pair
+  // same-step autoresets of a pair run outside the pair loop (the loop is left after a pair with
+  // a done env and re-entered): inside it their registers would spill the loop's to scratch
+  int it = 0;
+  for (;;) {
+    unsigned done = 0;
+    int de0 = 0;
+    for (; cur < np; ++it) {
+      R4<float>* cbuf = (it & 1) ? L.row1 : L.row0;
+      R4<float>* nbuf = (it & 1) ? L.row0 : L.row1;
+      const int e0 = eb + 2 * cur;
+      const bool hasB = 2 * cur + 1 < nbe;
+      const int kb = hasB ? 2 * cur + 1 : 2 * cur;
+      // records: wave-uniform LDS reads, moved to SGPRs
+      auto uni = [](float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); };
+      const R4<float> pa = rec[4 * cur], ma = rec[4 * cur + 1], pb = rec[2 * kb], mb = rec[2 * kb + 1];
+      const Pose2 PP{uni(pa.x), uni(pa.y), uni(pa.z), uni(pa.w), uni(pb.x), uni(pb.y), uni(pb.z), uni(pb.w)};
+      const int nA = (int)uni(ma.y), nB = hasB ? (int)uni(mb.y) : 0;
+      const unsigned trunc_m = (uni(ma.z) != 0.0f ? 1u : 0u) | (hasB && uni(mb.z) != 0.0f ? 2u : 0u);
+      const float part = (hasB && l >= 1) ? mb.x : ma.x;    // lane-per-env: lanes >= nb repeat
+      const int nxt = (int)__builtin_amdgcn_readlane(tk, 0);
+      if (S.prio) set_prio(3 - (4 * min(nxt, np)) / (np + 1));
+      if (nxt < np) {                                   // wave-uniform
+        if (l == 0) tk = atomicAdd(qctr, 1u);
+        dma_copy(S.obst + (size_t)(eb + 2 * nxt) * cap, nbuf, min(2, nbe - 2 * nxt) * rowb);
+      }
+      Scan<float> sa, sb;
+      lidar_wave2(reinterpret_cast<float4*>(cbuf), cap, nA, nB, PP, L.rayoff, L.slot, L.mark, sa, sb);
+      unsigned term_m = 0, coll_m = 0;
+      const int nb = hasB ? 2 : 1;
+      for (int k = 0; k < nb; ++k)
+        emit_env<float, MODE>(S, io, e0 + k, k ? sb : sa, (trunc_m >> k) & 1, k, term_m, coll_m);
+      {                                                 // lanes 0, 1 (lanes >= nb repeat)
+        const int k = min(l, nb - 1);
+        const bool coll = (coll_m >> k) & 1;            // simple_env.py:153-156
+        io.rew[e0 + k] = coll ? -20.0f + part : part;
+        io.term[e0 + k] = (term_m >> k) & 1;
+      }
+      // the next pair's rows landed: at least four stores (two sensor-row stores per env, the
+      // reward and the terminated flag) were issued after their DMA
+      vm_wait<4>();
+      cur = nxt;
+      if (S.autoreset == USV_AUTORESET_SAME_STEP && (term_m | trunc_m)) {
+        done = term_m | trunc_m;
+        de0 = e0;
+        ++it;
+        break;
+      }
+    }
+    if (!done) break;
+    for (; done; done &= done - 1) {
+      const int e = de0 + __builtin_ctz(done);
+      reset_wave<float, MODE>(S, e, io.obs + (size_t)e * kObsDim);
+    }
+  }
+  USV_STAMP_W(3);
+  USV_STAMP_W(6);
+}
+
+template <int MODE, bool FUSED>
+__global__ __launch_bounds__(kQBlock) __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8)))
+void step_q_kernel(State<float> S, IO<float> io) { step_q_body<MODE, FUSED>(S, io); }
 
 // 8 blocks of 256 threads per CU need <= 64 VGPRs and .sgpr_count <= 80 (MI355X_MICROARCH.md,
 // residency: 800 / (ceil(sgpr/16)*16 + 16) blocks; the occupancy API over-reports in 81..96).
@@ -1431,7 +1608,9 @@ struct Handle {
   // step-kernel variant (see launch_step; all variants give identical results):
   //   kind 0 = block kernel (one dynamics wave per block, barriers), 1 = fused wave kernel
   //   (step_kernel_wave), 2 = split (dyn_kernel + scan_kernel); epb = envs per 256-thread block
+  //   4 / 5 = block-queue step, split / fused (step_q_kernel; f32 window lidar, cap <= 32)
   int epb = 64, lid = 7, kind = 1;
+  int prio = 1;                        // scan loops raise the priority of lagging waves
   void* slab = nullptr;
   State<float> sf{};
   State<double> sd{};
@@ -1457,7 +1636,7 @@ int carve(Handle* h, State<R>& S) {
   const size_t bytes = F_NREAL * stride * sizeof(R) + al(I_NINT * stride * 4) +
                        al(N * cap * sizeof(R4<R>)) + al(N * kSensors * sizeof(R)) +
                        al((size_t)kAsmcN * N * sizeof(R)) + al((size_t)kV0N * stride * sizeof(R)) +
-                       al(2 * kSensors * sizeof(R)) + al(N * sizeof(R4<R>));
+                       al(2 * kSensors * sizeof(R)) + al(2 * N * sizeof(R4<R>));
   HIP_TRY(hipMalloc(&h->slab, bytes));
   HIP_TRY(hipMemset(h->slab, 0, bytes));
   char* p = (char*)h->slab;
@@ -1471,18 +1650,19 @@ int carve(Handle* h, State<R>& S) {
   S.v0 = (R*)take((size_t)kV0N * stride * sizeof(R));
   R* tab = (R*)take(2 * kSensors * sizeof(R));
   S.ray_tab = tab;
-  S.pose = (R4<R>*)take(N * sizeof(R4<R>));
+  S.pose = (R4<R>*)take(2 * N * sizeof(R4<R>));
   S.N = h->cfg.num_envs;
   S.cap = h->cfg.obstacle_cap;
   S.limit = h->cfg.max_episode_steps;
   S.autoreset = h->cfg.autoreset;
+  S.prio = h->prio;
   S.seed = h->cfg.seed;
   S.gid0 = h->cfg.env_id_offset;
   // ray offsets start + i*res (usv_asmc_ca_env.py:420), cos/sin in float64 on the host
   std::vector<R> ht(2 * kSensors);
   const double span = (2.0 / 3.0) * (2.0 * kPi), res = span / kSensors;
   for (int i = 0; i < kSensors; ++i) {
-    const double a = -kPi * 2.0 / 3.0 + i * res;
+    const double a = i * res;            // from ray 0 (heading - 120 deg): see to_ray0
     ht[2 * i] = (R)std::cos(a);          // interleaved (c, s): the LDS image, copied verbatim
     ht[2 * i + 1] = (R)std::sin(a);
   }
@@ -1575,6 +1755,22 @@ int launch_step(Handle* h, State<R>& S, const float* act, float* obs, void* rew,
   const int epb = h->epb, lid = h->lid;
   void* fn;
   size_t lds;
+  if constexpr (std::is_same<R, float>::value) {
+    if (h->kind == 4 || h->kind == 5) {                     // block-queue step
+      void* args[] = {(void*)&S, (void*)&io};
+      const bool simple = h->cfg.mode == USV_MODE_SIMPLE;
+      void* fn;
+      if (h->kind == 4) {
+        void* dyn = simple ? (void*)&dyn_kernel<R, USV_MODE_SIMPLE> : (void*)&dyn_kernel<R, USV_MODE_ASMC_SIMPLE>;
+        HIP_TRY(hipLaunchKernel(dyn, dim3((S.N + kBlock - 1) / kBlock), dim3(kBlock), args, 0, st));
+        fn = simple ? (void*)&step_q_kernel<USV_MODE_SIMPLE, false> : (void*)&step_q_kernel<USV_MODE_ASMC_SIMPLE, false>;
+      } else {
+        fn = simple ? (void*)&step_q_kernel<USV_MODE_SIMPLE, true> : (void*)&step_q_kernel<USV_MODE_ASMC_SIMPLE, true>;
+      }
+      HIP_TRY(hipLaunchKernel(fn, dim3((S.N + kQEnvs - 1) / kQEnvs), dim3(kQBlock), args, lds_q_bytes(S.cap), st));
+      return USV_OK;
+    }
+  }
   if (h->kind == 2 || h->kind == 3) {                       // split: dynamics, then scan
     void* args[] = {(void*)&S, (void*)&io};
     void* dyn = h->cfg.mode == USV_MODE_SIMPLE ? (void*)&dyn_kernel<R, USV_MODE_SIMPLE>
@@ -1805,11 +2001,19 @@ int usv_create(const usv_config* cfg, int32_t device, void** out) {
     const bool split_ok = ((kind == 2 && (epb == 4 || epb == 8 || epb == 16 || epb == 32)) ||
                            (kind == 3 && (epb == 1 || epb == 2 || epb == 4 || epb == 8))) &&
                           (lid == 0 || lid == 3 || lid == 7);
-    if (got >= 2 && (blk_ok || wave_ok || split_ok) && lid >= 0 && lid <= 7) {
+    const bool queue_ok = (kind == 4 || kind == 5) && lid == 7 && cfg->precision == USV_F32 && cfg->obstacle_cap <= 32;
+    if (got >= 2 && (blk_ok || wave_ok || split_ok || queue_ok) && lid >= 0 && lid <= 7) {
       h->epb = epb;
       h->lid = lid;
       h->kind = kind;
     }
+  }
+  if (const char* v = std::getenv("USV_PRIO")) h->prio = std::atoi(v);   // tuning override
+  if (h->kind == 4 || h->kind == 5) {   // the block-queue step's LDS exceeds the 64 KiB default
+    const int bytes = (int)lds_q_bytes(cfg->obstacle_cap);
+    for (void* fn : {(void*)&step_q_kernel<USV_MODE_SIMPLE, false>, (void*)&step_q_kernel<USV_MODE_SIMPLE, true>,
+                     (void*)&step_q_kernel<USV_MODE_ASMC_SIMPLE, false>, (void*)&step_q_kernel<USV_MODE_ASMC_SIMPLE, true>})
+      HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
   }
   const int rc = cfg->precision == USV_F32 ? carve<float>(h, h->sf) : carve<double>(h, h->sd);
   if (rc != USV_OK) {

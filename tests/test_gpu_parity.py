@@ -339,7 +339,8 @@ def test_step_variants_bit_identical(env_id, precision, monkeypatch):
             + torch.tensor([0.2, -1.0], device="cuda") for _ in range(T)]
     ref = None
     for v in ("64,0", "16,1", "32,3", "32,5", "32,7", "64,7", "32,0,1", "32,3,1", "16,7,1", "32,7,1", "64,7,1",
-              "16,0,2", "32,3,2", "4,7,2", "8,7,2", "16,7,2", "32,7,2", "1,7,3", "2,3,3", "4,7,3", "8,7,3"):
+              "16,0,2", "32,3,2", "4,7,2", "8,7,2", "16,7,2", "32,7,2", "1,7,3", "2,3,3", "4,7,3", "8,7,3",
+              "2,7,4", "2,7,5"):
         monkeypatch.setenv("USV_STEP_VARIANT", v)
         env = make(env_id, n, seed=4, precision=precision)
         env.reset(seed=4)
@@ -354,6 +355,33 @@ def test_step_variants_bit_identical(env_id, precision, monkeypatch):
         for t, (a_, b_) in enumerate(zip(ref, outs)):
             for x, y in zip(a_, b_):
                 assert torch.equal(x, y), f"variant {v} differs at step {t}"
+
+
+@pytest.mark.parametrize("n", [1, 77, 1077])
+def test_block_queue_ragged_sizes(n, monkeypatch):
+    """Block-queue step (kinds 4, 5: 128-env blocks of 16 waves pulling env pairs from an LDS
+    counter) on env counts that leave a partial block and an odd last pair: bit-identical to
+    the fused wave kernel over a rollout with resets."""
+    T = 40
+    gen = torch.Generator(device="cuda").manual_seed(5)
+    acts = [torch.rand(n, 2, device="cuda", generator=gen) * torch.tensor([0.8, 2.0], device="cuda")
+            + torch.tensor([0.2, -1.0], device="cuda") for _ in range(T)]
+    ref = None
+    for v in ("64,7,1", "2,7,5", "2,7,4"):
+        monkeypatch.setenv("USV_STEP_VARIANT", v)
+        env = make("usv-simple", n, seed=6, max_episode_steps=12)
+        env.reset(seed=6)
+        outs = []
+        for a in acts:
+            o, r, te, tr, info = env.step(a)
+            outs.append((o.clone(), r.clone(), te.clone(), tr.clone(), info["final_obs"].clone()))
+        env.close()
+        if ref is None:
+            ref = outs
+            continue
+        for t, (a_, b_) in enumerate(zip(ref, outs)):
+            for x, y in zip(a_, b_):
+                assert torch.equal(x, y), f"variant {v} differs at step {t} (n={n})"
 
 
 @pytest.mark.parametrize("precision", ["f32", "f64"])
@@ -373,7 +401,8 @@ def test_step_variants_bit_identical_scattered(precision, monkeypatch):
     assert far.mean() > 0.1, far.mean()          # the far path is actually exercised
     a = torch.from_numpy(rng.uniform([0.2, -1], [1, 1], size=(n, 2)).astype(np.float32)).cuda()
     ref = None
-    for v in ("64,0", "16,1", "32,3", "32,5", "32,7", "16,7", "32,3,1", "32,7,1", "64,7,1", "16,3,2", "8,7,2", "16,7,2", "2,7,3", "4,7,3"):
+    for v in ("64,0", "16,1", "32,3", "32,5", "32,7", "16,7", "32,3,1", "32,7,1", "64,7,1", "16,3,2", "8,7,2", "16,7,2", "2,7,3", "4,7,3",
+              "2,7,4", "2,7,5"):
         monkeypatch.setenv("USV_STEP_VARIANT", v)
         env = make("usv-simple", n, seed=3, precision=precision)
         inject(env, orc.env, elapsed=1)

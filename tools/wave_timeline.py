@@ -1,0 +1,95 @@
+"""Per-wave timeline of the fused wave kernel (kind 1) from the diagnostic build's stamps.
+
+    hipcc ... -DUSV_DIAG_STAMPS -o diag/stamps.so gym-usv_amd/csrc/usv_kernels.hip
+    USV_LIB_PATH=diag/stamps.so python tools/wave_timeline.py [--envs 65536] [--variant 16,7,1]
+
+Stamps (s_memrealtime, 100 MHz, per wave): 0 start, 1 dynamics done, 2 after the block barrier,
+3 scan done, 6 end; slot 7 = HW_ID | XCC_ID << 32.  Diagnostic only.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "gym-usv_amd")]
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def pct(v):
+    return np.percentile(v, [0, 10, 50, 90, 99, 100]).round(2).tolist()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--envs", type=int, default=65536)
+    ap.add_argument("--variant", default="16,7,1")
+    ap.add_argument("--warm", type=int, default=100)
+    ap.add_argument("--env-id", default="usv-simple")
+    args = ap.parse_args()
+    os.environ["USV_STEP_VARIANT"] = args.variant
+    import gym_usv_amd
+    lib = gym_usv_amd.load_library()
+    lib.usv_diag_stamps.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    env = gym_usv_amd.make_vec(args.env_id, args.envs, seed=1)
+    env.reset(seed=1)
+    g = torch.Generator(device="cuda").manual_seed(0)
+    lo, span = torch.tensor([0.2, -1.0], device="cuda"), torch.tensor([0.8, 2.0], device="cuda")
+    for _ in range(args.warm):
+        env.step(torch.rand(args.envs, 2, device="cuda", generator=g) * span + lo)
+    a = torch.rand(args.envs, 2, device="cuda", generator=g) * span + lo
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    env.step(a)
+    e1.record()
+    torch.cuda.synchronize()
+    epb = int(args.variant.split(",")[0])
+    nw = (args.envs + epb - 1) // epb * 4
+    buf = np.zeros(32768 * 8, dtype=np.uint64)
+    assert lib.usv_diag_stamps(buf.ctypes.data_as(ctypes.c_void_p), buf.nbytes) == 0
+    v = args.variant.split(",")
+    if len(v) > 2 and v[2] == "3":
+        nw = (args.envs + epb - 1) // epb          # one-wave blocks
+    if len(v) > 2 and v[2] in ("4", "5"):
+        nw = (args.envs + 127) // 128 * 16          # 16-wave blocks of 128 envs
+    raw = buf.reshape(32768, 8)[:nw].copy()
+    raw[raw[:, 2] == 0, 2] = raw[raw[:, 2] == 0, 1]   # scan kernels: no barrier stamp
+    st = raw[:, [0, 1, 2, 3, 6]].astype(np.int64)
+    t0 = st[:, 0].min()
+    st = (st - t0) / 100.0   # us
+    hw = raw[:, 7] & 0xFFFFFFFF
+    xcc = (raw[:, 7] >> 32) & 0xF
+    simd = (hw >> 4) & 3
+    cu = (hw >> 8) & 15
+    se = (hw >> 13) & 7
+    sid = ((xcc * 8 + se) * 16 + cu) * 4 + simd
+    out = {"envs": args.envs, "variant": args.variant, "waves": int(nw),
+           "event_us": round(e0.elapsed_time(e1) * 1e3, 2),
+           "span_us": float(st[:, 4].max()),
+           "start_us": pct(st[:, 0]), "end_us": pct(st[:, 4]),
+           "dyn_us": pct(st[:, 1] - st[:, 0]), "barrier_us": pct(st[:, 2] - st[:, 1]),
+           "scan_us": pct(st[:, 3] - st[:, 2]), "epi_us": pct(st[:, 4] - st[:, 3]),
+           "life_us": pct(st[:, 4] - st[:, 0]),
+           "distinct_simds": int(len(np.unique(sid)))}
+    # first-round waves (start within 1 us of t0) vs later ones
+    first = st[:, 0] < 1.0
+    out["first_round_waves"] = int(first.sum())
+    for nm, m in (("first", first), ("later", ~first)):
+        if m.any():
+            out[nm + "_dyn_us"] = round(float((st[m, 1] - st[m, 0]).mean()), 3)
+            out[nm + "_life_us"] = round(float((st[m, 4] - st[m, 0]).mean()), 3)
+    ts = np.linspace(0, st[:, 4].max(), 16)
+    out["alive_waves_over_time"] = [int(((st[:, 0] <= t) & (st[:, 4] > t)).sum()) for t in ts]
+    out["in_dyn_over_time"] = [int(((st[:, 0] <= t) & (st[:, 1] > t)).sum()) for t in ts]
+    out["in_scan_over_time"] = [int(((st[:, 2] <= t) & (st[:, 3] > t)).sum()) for t in ts]
+    _, per = np.unique(sid, return_counts=True)
+    out["waves_per_simd"] = pct(per)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
