@@ -1029,7 +1029,8 @@ __device__ __forceinline__ void scan_envs(const State<R>& S, const IO<R>& io, co
   const int iters = (ne + step - 1) / step;
   for (int k = 0; k < ne; k += step) {
     R4<R>* cur = ((k / step) & 1) ? L.row1 : L.row0;
-    if (S.prio) set_prio(3 - (4 * (k / step)) / iters);
+    if (S.prio == 1) set_prio(3 - (4 * (k / step)) / iters);
+    else if (S.prio == 2) set_prio(k + step >= ne ? 3 : 0);   // a wave's last iteration first
     prof.mark(4);
     // rows of this iteration landed: every env of the previous iteration issued its two
     // sensor-row stores after their DMA (a full pair: four), so all older ops are done
@@ -1104,7 +1105,7 @@ __device__ __forceinline__ void step_body_wave(const State<R>& S, const IO<R>& i
   Prof prof;
   USV_STAMP_W(0);
   USV_STAMP_ID();
-  if (S.prio) __builtin_amdgcn_s_setprio(3);
+  if (S.prio == 1) __builtin_amdgcn_s_setprio(3);
   scan_prologue<R, LID>(S, L, wave, e0, ne);
   // dynamics: lanes 0..ne-1; lanes >= ne recompute env ne-1 and store identical values to the
   // identical addresses (benign) -- no divergent memory operations, so hipcc's own vmcnt
@@ -1303,7 +1304,8 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
       const unsigned trunc_m = (uni(ma.z) != 0.0f ? 1u : 0u) | (hasB && uni(mb.z) != 0.0f ? 2u : 0u);
       const float part = (hasB && l >= 1) ? mb.x : ma.x;    // lane-per-env: lanes >= nb repeat
       const int nxt = (int)__builtin_amdgcn_readlane(tk, 0);
-      if (S.prio) set_prio(3 - (4 * min(nxt, np)) / (np + 1));
+      if (S.prio == 1) set_prio(3 - (4 * min(nxt, np)) / (np + 1));
+      else if (S.prio == 2) set_prio(nxt >= np ? 3 : 0);     // the block's last pairs first
       if (nxt < np) {                                   // wave-uniform
         if (l == 0) tk = atomicAdd(qctr, 1u);
         dma_copy(S.obst + (size_t)(eb + 2 * nxt) * cap, nbuf, min(2, nbe - 2 * nxt) * rowb);
@@ -1989,10 +1991,13 @@ int usv_create(const usv_config* cfg, int32_t device, void** out) {
   h->device = device;
   h->lid = cfg->lidar_algo == USV_LIDAR_BRUTE ? (kLidSkip | kLidUnroll2) : (kLidSkip | kLidUnroll2 | kLidWindow);
   // tuned defaults at 65 536 envs on MI355X (tools/sweep_variants.py, profiles/): usv-simple
-  // runs the fused wave kernel at 16 envs/wave; usv-asmc-simple the split step (its 20-substep
-  // dynamics want full 64-lane waves) at 4 envs/wave
+  // (f32, window lidar) runs the fused block-queue step, else the fused wave kernel at 16
+  // envs/wave; usv-asmc-simple the split step (its 20-substep dynamics want full 64-lane waves)
+  // at 4 envs/wave
   if (cfg->mode == USV_MODE_ASMC_SIMPLE) { h->kind = 2; h->epb = 16; }
-  else { h->kind = 1; h->epb = 64; }
+  else if (cfg->precision == USV_F32 && cfg->lidar_algo == USV_LIDAR_WINDOW && cfg->obstacle_cap <= 32) {
+    h->kind = 5; h->epb = 2;            // block-queue step
+  } else { h->kind = 1; h->epb = 64; }
   if (const char* v = std::getenv("USV_STEP_VARIANT")) {   // "epb,lid[,kind]" tuning override
     int epb = 0, lid = 0, kind = 0;
     const int got = std::sscanf(v, "%d,%d,%d", &epb, &lid, &kind);
@@ -2008,6 +2013,7 @@ int usv_create(const usv_config* cfg, int32_t device, void** out) {
       h->kind = kind;
     }
   }
+  h->prio = (h->kind == 4 || h->kind == 5) ? 0 : 1;   // the ramp helps static splits only
   if (const char* v = std::getenv("USV_PRIO")) h->prio = std::atoi(v);   // tuning override
   if (h->kind == 4 || h->kind == 5) {   // the block-queue step's LDS exceeds the 64 KiB default
     const int bytes = (int)lds_q_bytes(cfg->obstacle_cap);

@@ -88,6 +88,13 @@ def main():
     out["in_scan_over_time"] = [int(((st[:, 2] <= t) & (st[:, 3] > t)).sum()) for t in ts]
     _, per = np.unique(sid, return_counts=True)
     out["waves_per_simd"] = pct(per)
+    out["end_us_by_xcc"] = {int(x): [round(float(st[xcc == x, 4].mean()), 2), round(float(st[xcc == x, 4].max()), 2)]
+                            for x in np.unique(xcc)}
+    out["scan_us_by_xcc"] = {int(x): round(float((st[xcc == x, 3] - st[xcc == x, 2]).mean()), 2) for x in np.unique(xcc)}
+    wpb = 16 if (len(v) > 2 and v[2] in ("4", "5")) else (1 if (len(v) > 2 and v[2] == "3") else 4)
+    blk = st[: (nw // wpb) * wpb, 4].reshape(-1, wpb)
+    out["block_end_spread_us"] = pct(blk.max(1) - blk.min(1))
+    out["block_end_us"] = pct(blk.max(1))
     print(json.dumps(out))
 
 
