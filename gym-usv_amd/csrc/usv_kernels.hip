@@ -14,6 +14,7 @@
 // Reference: see include/usv_hip.h for the file:line each entry point replaces.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <type_traits>
 #include <cstdlib>
@@ -1230,14 +1231,18 @@ __global__ __launch_bounds__(kWave * WPB) void scan_kernel(State<R> S, IO<R> io)
 //   kind 4 (split): dyn_kernel ran first and left them in S.pose; they are DMA'd into LDS.
 // Each wave's first pair is static (pair = wave); its rows and the next pair's are DMA'd while
 // the current pair is scanned.
-constexpr int kQWaves = 16, kQBlock = kQWaves * kWave, kQEnvs = 128;
-__host__ __device__ constexpr size_t lds_q_bytes(int cap) {
-  return wave_tab_bytes<float>() + kQWaves * lds_scan_slice<float>(cap) + kQEnvs * 2 * 16 + 16;
+// QW waves per block, QE envs per block (QE / 64 waves run the dynamics): (8, 64), (16, 128), or
+// (16, 256) padded past 80 KiB of LDS so that exactly one block fits a CU -- then one queue
+// balances the whole CU and no block is starved by an older one on the same SIMDs.
+__host__ __device__ constexpr size_t lds_q_bytes(int cap, int qw, int qe) {
+  return std::max(wave_tab_bytes<float>() + qw * lds_scan_slice<float>(cap) + qe * 2 * 16 + 16,
+                  qe > 8 * qw ? (size_t)82 * 1024 : (size_t)0);
 }
 
-template <int MODE, bool FUSED>
+template <int MODE, bool FUSED, int QW, int QE>
 __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<float>& io) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
+  constexpr int kQWaves = QW, kQEnvs = QE;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const int l = lane_id();
   const int cap = S.cap, rowb = cap * (int)sizeof(float4);
@@ -1256,8 +1261,11 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
   int cur = wave;
   if (cur < np) dma_copy(S.obst + (size_t)(eb + 2 * cur) * cap, L.row0, min(2, nbe - 2 * cur) * rowb);
   if constexpr (FUSED) {
-    if (wave < kQEnvs / kWave) {                        // phase 1: dynamics, one lane per env
-      const int k = min(wave * kWave + l, nbe - 1);     // lanes past the end repeat the last env
+    // phase 1: dynamics, one lane per env.  Lanes past the end repeat the wave's last env (same
+    // wave: every lane loads the state before any lane stores it); a wave with no env of its
+    // own must not run, or two waves would race on the same env's state
+    if (wave < kQEnvs / kWave && wave * kWave < nbe) {
+      const int k = min(wave * kWave + l, nbe - 1);
       const int e = eb + k;
       const float2 a = reinterpret_cast<const float2*>(io.act)[e];
       float hdr[kHdr];
@@ -1272,14 +1280,17 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
       rec[2 * k + 1] = R4<float>{partial, (float)S.I(I_NOBS)[e], trunc ? 1.0f : 0.0f, 0.0f};
     }
   } else {
-    static_assert(kQEnvs == 2 * kWave, "waves 0 and 1 copy 64 records (2 KiB) each");
-    if (wave < 2 && wave * kWave < nbe)
+    if (wave < kQEnvs / kWave && wave * kWave < nbe)    // 64 records (2 KiB) per wave
       dma_copy(S.pose + 2 * (size_t)(eb + wave * kWave), rec + 2 * wave * kWave, min(kWave, nbe - wave * kWave) * 32);
   }
   // rows, ray table and records landed; the dynamics' header stores are complete before the
   // barrier, so a done env's terminal obs can copy its header from the obs row
   USV_STAMP_W(1);
+#ifdef USV_DIAG_NOSTOREWAIT   // diagnostic timing only: header stores may still be in flight
+  vm_wait<8>();
+#else
   vm_wait<0>();
+#endif
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   USV_STAMP_W(2);
   unsigned tk = 0;
@@ -1343,9 +1354,9 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
   USV_STAMP_W(6);
 }
 
-template <int MODE, bool FUSED>
-__global__ __launch_bounds__(kQBlock) __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8)))
-void step_q_kernel(State<float> S, IO<float> io) { step_q_body<MODE, FUSED>(S, io); }
+template <int MODE, bool FUSED, int QW, int QE>
+__global__ __launch_bounds__(QW * kWave) __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8)))
+void step_q_kernel(State<float> S, IO<float> io) { step_q_body<MODE, FUSED, QW, QE>(S, io); }
 
 // 8 blocks of 256 threads per CU need <= 64 VGPRs and .sgpr_count <= 80 (MI355X_MICROARCH.md,
 // residency: 800 / (ceil(sgpr/16)*16 + 16) blocks; the occupancy API over-reports in 81..96).
@@ -1745,6 +1756,19 @@ void* pick_scan(int epw, int lid) {
   return pick_scan_lid<R, MODE, 4, WPB>(lid);
 }
 
+template <int QW, int QE>
+void* pick_q_mode(int mode, bool fused) {
+  const bool simple = mode == USV_MODE_SIMPLE;
+  if (fused) return simple ? (void*)&step_q_kernel<USV_MODE_SIMPLE, true, QW, QE> : (void*)&step_q_kernel<USV_MODE_ASMC_SIMPLE, true, QW, QE>;
+  return simple ? (void*)&step_q_kernel<USV_MODE_SIMPLE, false, QW, QE> : (void*)&step_q_kernel<USV_MODE_ASMC_SIMPLE, false, QW, QE>;
+}
+int q_waves(int qe) { return qe == 64 ? 8 : 16; }
+void* pick_q(int mode, bool fused, int qe) {
+  if (qe == 64) return pick_q_mode<8, 64>(mode, fused);
+  if (qe == 256) return pick_q_mode<16, 256>(mode, fused);
+  return pick_q_mode<16, 128>(mode, fused);
+}
+
 template <typename R>
 int launch_step(Handle* h, State<R>& S, const float* act, float* obs, void* rew, uint8_t* term,
                 uint8_t* trunc, float* fobs, hipStream_t st) {
@@ -1758,18 +1782,17 @@ int launch_step(Handle* h, State<R>& S, const float* act, float* obs, void* rew,
   void* fn;
   size_t lds;
   if constexpr (std::is_same<R, float>::value) {
-    if (h->kind == 4 || h->kind == 5) {                     // block-queue step
+    if (h->kind == 4 || h->kind == 5) {                     // block-queue step, epb envs per block
       void* args[] = {(void*)&S, (void*)&io};
       const bool simple = h->cfg.mode == USV_MODE_SIMPLE;
-      void* fn;
+      const int qw = q_waves(h->epb);
       if (h->kind == 4) {
         void* dyn = simple ? (void*)&dyn_kernel<R, USV_MODE_SIMPLE> : (void*)&dyn_kernel<R, USV_MODE_ASMC_SIMPLE>;
         HIP_TRY(hipLaunchKernel(dyn, dim3((S.N + kBlock - 1) / kBlock), dim3(kBlock), args, 0, st));
-        fn = simple ? (void*)&step_q_kernel<USV_MODE_SIMPLE, false> : (void*)&step_q_kernel<USV_MODE_ASMC_SIMPLE, false>;
-      } else {
-        fn = simple ? (void*)&step_q_kernel<USV_MODE_SIMPLE, true> : (void*)&step_q_kernel<USV_MODE_ASMC_SIMPLE, true>;
       }
-      HIP_TRY(hipLaunchKernel(fn, dim3((S.N + kQEnvs - 1) / kQEnvs), dim3(kQBlock), args, lds_q_bytes(S.cap), st));
+      void* fn = pick_q(h->cfg.mode, h->kind == 5, h->epb);
+      HIP_TRY(hipLaunchKernel(fn, dim3((S.N + h->epb - 1) / h->epb), dim3(qw * kWave), args,
+                              lds_q_bytes(S.cap, qw, h->epb), st));
       return USV_OK;
     }
   }
@@ -1996,7 +2019,7 @@ int usv_create(const usv_config* cfg, int32_t device, void** out) {
   // at 4 envs/wave
   if (cfg->mode == USV_MODE_ASMC_SIMPLE) { h->kind = 2; h->epb = 16; }
   else if (cfg->precision == USV_F32 && cfg->lidar_algo == USV_LIDAR_WINDOW && cfg->obstacle_cap <= 32) {
-    h->kind = 5; h->epb = 2;            // block-queue step
+    h->kind = 5; h->epb = 128;          // block-queue step, 16-wave blocks
   } else { h->kind = 1; h->epb = 64; }
   if (const char* v = std::getenv("USV_STEP_VARIANT")) {   // "epb,lid[,kind]" tuning override
     int epb = 0, lid = 0, kind = 0;
@@ -2006,7 +2029,8 @@ int usv_create(const usv_config* cfg, int32_t device, void** out) {
     const bool split_ok = ((kind == 2 && (epb == 4 || epb == 8 || epb == 16 || epb == 32)) ||
                            (kind == 3 && (epb == 1 || epb == 2 || epb == 4 || epb == 8))) &&
                           (lid == 0 || lid == 3 || lid == 7);
-    const bool queue_ok = (kind == 4 || kind == 5) && lid == 7 && cfg->precision == USV_F32 && cfg->obstacle_cap <= 32;
+    const bool queue_ok = (kind == 4 || kind == 5) && (epb == 64 || epb == 128 || epb == 256) && lid == 7 &&
+                          cfg->precision == USV_F32 && cfg->obstacle_cap <= 32;
     if (got >= 2 && (blk_ok || wave_ok || split_ok || queue_ok) && lid >= 0 && lid <= 7) {
       h->epb = epb;
       h->lid = lid;
@@ -2015,11 +2039,9 @@ int usv_create(const usv_config* cfg, int32_t device, void** out) {
   }
   h->prio = (h->kind == 4 || h->kind == 5) ? 0 : 1;   // the ramp helps static splits only
   if (const char* v = std::getenv("USV_PRIO")) h->prio = std::atoi(v);   // tuning override
-  if (h->kind == 4 || h->kind == 5) {   // the block-queue step's LDS exceeds the 64 KiB default
-    const int bytes = (int)lds_q_bytes(cfg->obstacle_cap);
-    for (void* fn : {(void*)&step_q_kernel<USV_MODE_SIMPLE, false>, (void*)&step_q_kernel<USV_MODE_SIMPLE, true>,
-                     (void*)&step_q_kernel<USV_MODE_ASMC_SIMPLE, false>, (void*)&step_q_kernel<USV_MODE_ASMC_SIMPLE, true>})
-      HIP_TRY(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  if (h->kind == 4 || h->kind == 5) {   // the block-queue step's LDS can exceed the 64 KiB default
+    HIP_TRY(hipFuncSetAttribute(pick_q(cfg->mode, h->kind == 5, h->epb), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds_q_bytes(cfg->obstacle_cap, q_waves(h->epb), h->epb)));
   }
   const int rc = cfg->precision == USV_F32 ? carve<float>(h, h->sf) : carve<double>(h, h->sd);
   if (rc != USV_OK) {

@@ -55,7 +55,7 @@ def main():
     if len(v) > 2 and v[2] == "3":
         nw = (args.envs + epb - 1) // epb          # one-wave blocks
     if len(v) > 2 and v[2] in ("4", "5"):
-        nw = (args.envs + 127) // 128 * 16          # 16-wave blocks of 128 envs
+        nw = (args.envs + epb - 1) // epb * (8 if epb == 64 else 16)   # block-queue blocks
     raw = buf.reshape(32768, 8)[:nw].copy()
     raw[raw[:, 2] == 0, 2] = raw[raw[:, 2] == 0, 1]   # scan kernels: no barrier stamp
     st = raw[:, [0, 1, 2, 3, 6]].astype(np.int64)
@@ -91,7 +91,7 @@ def main():
     out["end_us_by_xcc"] = {int(x): [round(float(st[xcc == x, 4].mean()), 2), round(float(st[xcc == x, 4].max()), 2)]
                             for x in np.unique(xcc)}
     out["scan_us_by_xcc"] = {int(x): round(float((st[xcc == x, 3] - st[xcc == x, 2]).mean()), 2) for x in np.unique(xcc)}
-    wpb = 16 if (len(v) > 2 and v[2] in ("4", "5")) else (1 if (len(v) > 2 and v[2] == "3") else 4)
+    wpb = (8 if epb == 64 else 16) if (len(v) > 2 and v[2] in ("4", "5")) else (1 if (len(v) > 2 and v[2] == "3") else 4)
     blk = st[: (nw // wpb) * wpb, 4].reshape(-1, wpb)
     out["block_end_spread_us"] = pct(blk.max(1) - blk.min(1))
     out["block_end_us"] = pct(blk.max(1))
