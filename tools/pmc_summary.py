@@ -15,6 +15,10 @@ import csv
 import glob
 import json
 import os
+import re
+
+# every step-kernel family: step_kernel, step_kernel_wave, step_q_kernel, scan_kernel (split step)
+STEP_RE = re.compile(r"usv::(step\w*_kernel|scan_kernel)")
 
 
 def rows(d, pattern):
@@ -24,9 +28,11 @@ def rows(d, pattern):
     return list(csv.DictReader(open(f[0])))
 
 
-def counter(d, name, kernel="step_kernel", skip=5):
+def counter(d, name, skip=5):
     vals = [float(r["Counter_Value"]) for r in rows(d, "*counter_collection.csv")
-            if kernel in r["Kernel_Name"] and r["Counter_Name"] == name]
+            if STEP_RE.search(r["Kernel_Name"]) and r["Counter_Name"] == name]
+    if not vals:
+        raise SystemExit(f"no step-kernel {name} samples under {d}")
     vals = vals[skip:] or vals
     return sum(vals) / len(vals), len(vals)
 
@@ -41,13 +47,14 @@ def main():
     ap.add_argument("--out", default="profiles")
     a = ap.parse_args()
     stats = [r for r in rows(a.kt, "*kernel_stats.csv") if "usv::" in r["Name"]]
-    step = [r for r in stats if "step_kernel" in r["Name"]]
+    step = [r for r in stats if STEP_RE.search(r["Name"])]
     fetch_kib, nf = counter(a.fetch, "FETCH_SIZE")
     write_kib, nw = counter(a.write, "WRITE_SIZE")
     summ = {
         "key": a.key,
         "kernel_stats": [{k: r[k] for k in ("Name", "Calls", "AverageNs", "MinNs", "MaxNs", "Percentage")}
                          for r in stats[:8]],
+        "step_kernel": step[0]["Name"] if step else None,
         "step_kernel_avg_ns": float(step[0]["AverageNs"]) if step else None,
         "fetch_kib_per_launch": fetch_kib, "write_kib_per_launch": write_kib,
         "fetch_samples": nf, "write_samples": nw,
