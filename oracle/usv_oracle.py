@@ -634,3 +634,179 @@ class AsmcV0Batch:
         self.last = np.stack([q(xd), q(yd), q(pd), q(ud), q(vd), q(rd), q(e_u_last), q(kdu), q(kdp)], axis=1)
         self.first[:] = False
         return self.state.astype(np.float32), reward, done
+
+
+# --------------------------------------------------------------------------- legacy float64 family
+PID_KP_U, PID_KI_U, PID_KD_U, PID_KP_PSI, PID_KD_PSI = 1.1, 0.2, 0.1, 0.8, 3.0   # usv_pid_env.py:40-44
+YE_INT_K_I = 0.001                                                               # usv_asmc_ye_int_env.py:51
+LEGACY_MAX_YE, LEGACY_MIN_X = 10.0, -10.0    # usv_asmc_ye_int_env.py:63,78 / usv_pid_env.py:60
+
+
+class LegacyF64Batch:
+    """Batched restatement of the float64 legacy path-following envs built on the usv-asmc-v0
+    template:
+
+    * ``family="ye_int"`` -- ``UsvAsmcYeIntEnv`` (id usv-asmc-ye-int-v0,
+      usv_asmc_ye_int_env.py:92-253): the usv-asmc-v0 ASMC + plant step in float64 (no float32
+      arrays), plus a cross-track integral that restarts when ye changes sign (:230-235); the
+      obs carries ye_ss = ye + k_i * ye_int (:235, :247); reward r_act + (exp(-k_ye |ye|) or
+      the heading penalty) (:350-360); reset ranges x, y ~ U(-5, 5), speed ~ U(0.4, 1.4)
+      (:256-296).
+    * ``family="pid"`` -- ``UsvPidEnv`` (id usv-pid-v0, usv_pid_env.py:89-233): the same plant
+      driven by a PID surge/heading law (:148-155; e_u_last is never updated, so e_u_dot =
+      e_u / h), the usv-asmc-v0 reward (:329-338), reset ranges as usv-asmc-v0 but speed ~
+      U(0.4, 1.4) (:236-276).
+
+    Both end an episode when |ye| > 10 or x < -10 with reward -1 (ye_int :241-245, pid
+    :219-223).  The state is float64 throughout; only ``ak`` and the reset ``psi_ak`` are
+    rounded to float32 (ye_int :282-286, pid :260-264).  Citations below are
+    usv_asmc_ye_int_env.py lines; usv_pid_env.py has the same statements 4 (step) or
+    20 (reset) lines earlier.  Actions are float32 scalars (promoted to float64 against the
+    float64 state).  Resets draw from a per-env ``np.random.RandomState`` in the reference order.
+    """
+
+    obs_dim = 6
+    act_dim = 1
+
+    def __init__(self, n, family):
+        assert family in ("ye_int", "pid")
+        self.n, self.family = n, family
+        z = lambda *s: np.zeros((n,) + s)
+        self.velocity, self.position = z(3), z(3)
+        self.aux = z(4)             # e_u_int, Ka_u, Ka_psi, ye_int (ye_int: ye-int env only)
+        self.last = z(10)           # eta_dot_last(3), upsilon_dot_last(3), e_u_last, Ka_dot_u/psi_last, ye_last
+        self.target = z(6)          # x_0, y_0, desired_speed, ak, x_d, y_d
+        self.state = z(6)
+        self.rngs = [None] * n
+
+    def reset_env(self, i, seed=None):
+        if seed is not None or self.rngs[i] is None:
+            self.rngs[i] = np.random.RandomState(seed)
+        g = self.rngs[i]
+        lim = 5.0 if self.family == "ye_int" else 2.5
+        x, y = g.uniform(-lim, lim), g.uniform(-lim, lim)                  # :258-259
+        psi = g.uniform(-np.pi, np.pi)
+        x0, y0 = g.uniform(-2.5, 2.5), g.uniform(-2.5, 2.5)
+        xd = g.uniform(15, 30)
+        yd = y0
+        ds = g.uniform(0.4, 1.4)                                           # :279
+        ak = float(f32(math.atan2(yd - y0, xd - x0)))                      # :281-282
+        psi_ak = float(f32(wrap_once(np.float64(psi - ak))))              # :284-286
+        ye = -(x - x0) * math.sin(ak) + (y - y0) * math.cos(ak)            # :287-288
+        self.velocity[i] = 0.0
+        self.position[i] = [x, y, psi]
+        self.aux[i] = 0.0
+        self.last[i] = 0.0
+        self.target[i] = [x0, y0, ds, ak, xd, yd]
+        self.state[i] = [0.0, 0.0, 0.0, ye, psi_ak, 0.0]                   # body_to_path(0, 0) = 0 (:289-291)
+
+    def reset(self, seeds=None, idx=None):
+        idx = range(self.n) if idx is None else idx
+        for k, i in enumerate(idx):
+            self.reset_env(i, None if seeds is None else seeds[k])
+        return self.state.astype(np.float32)
+
+    def step(self, action):
+        """action [N] heading offsets (float32); returns obs [N,6] f32, reward [N], done [N]."""
+        a = np.asarray(action, dtype=np.float32).reshape(self.n).astype(np.float64)
+        u, v, r = (self.velocity[:, k] for k in range(3))
+        x, y, psi = (self.position[:, k] for k in range(3))
+        e_u_int, ka_u, ka_psi, ye_int = (self.aux[:, k] for k in range(4))
+        xd_l, yd_l, pd_l, ud_l, vd_l, rd_l, e_u_last, kdu_l, kdp_l, ye_last = (self.last[:, k] for k in range(10))
+        x0, y0, ds, ak = (self.target[:, k] for k in range(4))
+        action_dot = (a - self.state[:, 5]) / H                            # :113
+        psi_d = wrap_once(a + ak)                                          # :116-117
+        fast = np.abs(u) > 1.2                                             # :119-123
+        xu = np.where(fast, 64.55, -25.0)
+        xuu = np.where(fast, -70.92, 0.0)
+        mag = np.sqrt(np.power(u, 2) + np.power(v, 2))
+        yv = 0.5 * (-40 * 1000 * np.abs(v)) * (1.1 + 0.0045 * (1.01 / 0.09) - 0.1 * (0.27 / 0.09) + 0.016 * np.power((0.27 / 0.09), 2))
+        yr = 6 * (-3.141592 * 1000) * mag * 0.09 * 0.09 * 1.01            # :125-132
+        nv = 0.06 * (-3.141592 * 1000) * mag * 0.09 * 0.09 * 1.01
+        nr = 0.02 * (-3.141592 * 1000) * mag * 0.09 * 0.09 * 1.01 * 1.01
+        g_u, g_psi = 1 / (MASS - X_U_DOT), 1 / (IZ - N_R_DOT)              # :134-138
+        f_u = ((MASS - Y_V_DOT) * v * r + (xuu * np.abs(u) + xu * u)) / (MASS - X_U_DOT)
+        f_psi = ((-X_U_DOT + Y_V_DOT) * u * v + (nr * r)) / (IZ - N_R_DOT)
+        e_psi = wrap_once(psi_d - psi)                                     # :140-152
+        e_psi_dot = 0 - r
+        u_psi = 1 / (1 + np.exp(10 * (np.abs(e_psi) * (2 / np.pi) - 0.5)))
+        u_d = (ds - V0_MIN_SPEED) * u_psi + V0_MIN_SPEED
+        e_u = u_d - u
+        e_u_int = H * (e_u + e_u_last) / 2 + e_u_int
+        if self.family == "ye_int":                                        # ASMC, :154-170
+            sig_u = e_u + LAMBDA_U * e_u_int
+            sig_p = e_psi_dot + LAMBDA_PSI * e_psi
+            kdu = np.where(ka_u > KMIN_U, K_U * np.sign(np.abs(sig_u) - MU_U), KMIN_U)
+            kdp = np.where(ka_psi > KMIN_PSI, K_PSI * np.sign(np.abs(sig_p) - MU_PSI), KMIN_PSI)
+            ka_u = H * (kdu + kdu_l) / 2 + ka_u
+            ka_psi = H * (kdp + kdp_l) / 2 + ka_psi
+            ua_u = (-ka_u * np.power(np.abs(sig_u), 0.5) * np.sign(sig_u)) - (K2_U * sig_u)
+            ua_p = (-ka_psi * np.power(np.abs(sig_p), 0.5) * np.sign(sig_p)) - (K2_PSI * sig_p)
+            tx = ((LAMBDA_U * e_u) - f_u - ua_u) / g_u
+            tz = ((LAMBDA_PSI * e_psi) - f_psi - ua_p) / g_psi
+        else:                                                              # PID, usv_pid_env.py:149-155
+            kdu, kdp = kdu_l, kdp_l
+            e_u_dot = (e_u - e_u_last) / H
+            ua_u = (PID_KP_U * e_u) + (PID_KI_U * e_u_int) + (PID_KD_U * e_u_dot)
+            ua_p = (PID_KP_PSI * e_psi) + (PID_KD_PSI * e_psi_dot)
+            tx = (-f_u + ua_u) / g_u
+            tz = (-f_psi + ua_p) / g_psi
+        tport = tx / 2 + tz / B_TH                                         # :172-178
+        tstbd = tx / (2 * C_TH) - tz / (B_TH * C_TH)
+        tport = np.where(tport > 36.5, 36.5, tport)
+        tport = np.where(tport < -30, -30.0, tport)
+        tstbd = np.where(tstbd > 36.5, 36.5, tstbd)
+        tstbd = np.where(tstbd < -30, -30.0, tstbd)
+        t0 = tport + C_TH * tstbd                                          # :184
+        t2 = 0.5 * B_TH * (tport - C_TH * tstbd)
+        # C = CRB + CA, D = Dl - Dn (:186-205); only their non-zero entries enter C nu, D nu
+        c02 = (0 - MASS * v) + 2 * ((Y_V_DOT * v) + ((Y_R_DOT + N_V_DOT) / 2) * r)
+        c12 = (MASS * u) + (0 - X_U_DOT * MASS * u)
+        c20 = (MASS * v) + 2 * (((0 - Y_V_DOT) * v) - ((Y_R_DOT + N_V_DOT) / 2) * r)
+        c21 = (0 - MASS * u) + (X_U_DOT * MASS * u)
+        av, ar = np.abs(v), np.abs(r)
+        d00 = (0 - xu) - xuu * np.abs(u)
+        d11 = (0 - yv) - (YVV * av + YVR * ar)
+        d12 = (0 - yr) - (YRV * av + YRR * ar)
+        d21 = (0 - nv) - (NVV * av + NVR * ar)
+        d22 = (0 - nr) - (NRV * av + NRR * ar)
+        rhs0 = (t0 - c02 * r) - d00 * u                                    # :207-208
+        rhs1 = (0 - c12 * r) - (d11 * v + d12 * r)
+        rhs2 = (t2 - (c20 * u + c21 * v)) - (d21 * v + d22 * r)
+        ud = M_INV[0, 0] * rhs0 + M_INV[0, 1] * rhs1 + M_INV[0, 2] * rhs2
+        vd = M_INV[1, 0] * rhs0 + M_INV[1, 1] * rhs1 + M_INV[1, 2] * rhs2
+        rd = M_INV[2, 0] * rhs0 + M_INV[2, 1] * rhs1 + M_INV[2, 2] * rhs2
+        u = H * (ud + ud_l) / 2 + u                                        # :209-211
+        v = H * (vd + vd_l) / 2 + v
+        r = H * (rd + rd_l) / 2 + r
+        cj, sj = np.cos(psi), np.sin(psi)                                  # J(psi) :213-215
+        xd, yd, pd = cj * u - sj * v, sj * u + cj * v, r
+        x = H * (xd + xd_l) / 2 + x                                        # :217-219
+        y = H * (yd + yd_l) / 2 + y
+        psi = wrap_once(H * (pd + pd_l) / 2 + psi)                         # :221-222
+        psi_ak = wrap_once(psi - ak)                                       # :224-225
+        ye = -(x - x0) * np.sin(ak) + (y - y0) * np.cos(ak)               # :227
+        ye_abs = np.abs(ye)
+        pa = np.abs(psi_ak)
+        r_act = V0_W_ACTION * np.tanh(-V0_C_ACTION * np.power(action_dot, 2))
+        r_ak = -np.exp(V0_K_AK * (pa - np.pi))
+        if self.family == "ye_int":
+            ye_int = np.where(np.sign(ye) != np.sign(ye_last), 0.0, ye_int)   # :230-232
+            ye_int = H * (ye + ye_last) + ye_int
+            ye_last = ye
+            ye_obs = ye + YE_INT_K_I * ye_int                              # ye_ss (:235)
+            reward = r_act + np.where(pa < np.pi / 2, np.exp(-V0_K_YE * ye_abs), r_ak)   # :350-360
+        else:
+            ye_obs = ye
+            r_ye = np.where(ye_abs > V0_SIGMA_YE, np.exp(-V0_K_YE * ye_abs),
+                            np.exp(-V0_K_YE * np.power(ye_abs, 2) / V0_SIGMA_YE))
+            reward = np.where(pa < np.pi / 2, r_act + r_ye, r_ak)         # usv_pid_env.py:329-338
+        v_ak = np.sin(psi_ak) * u + np.cos(psi_ak) * v                     # body_to_path :239, :362-376
+        done = (ye_abs > LEGACY_MAX_YE) | (x < LEGACY_MIN_X)                # :241-245
+        reward = np.where(done, -1.0, reward)
+        self.state = np.stack([u, v_ak, r, ye_obs, psi_ak, a], axis=1)
+        self.velocity = np.stack([u, v, r], axis=1)
+        self.position = np.stack([x, y, psi], axis=1)
+        self.aux = np.stack([e_u_int, ka_u, ka_psi, ye_int], axis=1)
+        self.last = np.stack([xd, yd, pd, ud, vd, rd, e_u_last, kdu, kdp, ye_last], axis=1)
+        return self.state.astype(np.float32), reward, done

@@ -14,6 +14,9 @@ reference source travels.  Fixtures:
                             TimeLimit + same-step autoreset (SB3 DummyVecEnv semantics).
 * ``asmc_simple_traj.npz`` -- the same for UsvSimpleASMCEnv (usv-asmc-simple).
 * ``asmc_v0_traj.npz``   -- legacy UsvAsmcEnv (usv-asmc-v0) seeded rollouts with resets on done.
+* ``asmc_ye_int_traj.npz`` / ``pid_traj.npz`` -- the float64 legacy envs UsvAsmcYeIntEnv
+                            (usv-asmc-ye-int-v0) and UsvPidEnv (usv-pid-v0), same protocol
+                            (``python tests/golden/make_golden.py --legacy-f64`` makes only these).
 """
 from __future__ import annotations
 
@@ -186,9 +189,50 @@ def gen_asmc_v0(E, fname="asmc_v0_traj.npz", n_env=4, T=3000):
     print(fname, "episodes ended:", int(done.sum()))
 
 
+def gen_legacy_f64(E, cls, fname, n_env=4, T=2000, seed0=3000):
+    """Legacy float64 path-following envs on the usv-asmc-v0 template: UsvAsmcYeIntEnv
+    (usv-asmc-ye-int-v0, usv_asmc_ye_int_env.py:92-296) and UsvPidEnv (usv-pid-v0,
+    usv_pid_env.py:89-278).  Same protocol as gen_asmc_v0: per-env np.random.seed, float32
+    scalar actions, reset on done; the reference's obs are float64, stored here as float32 (the
+    Box dtype, and what the C-ABI returns)."""
+    rng = np.random.default_rng(seed0)
+    acts = rng.uniform(-np.pi / 2, np.pi / 2, size=(n_env, T))
+    # envs 1.. hold a heading offset near +-pi/2 so |ye| passes 10 within the rollout
+    for e in range(1, n_env):
+        acts[e] = np.clip(rng.normal((-1) ** e * (1.2 + 0.1 * e), 0.15, size=T), -np.pi / 2, np.pi / 2)
+    acts = acts.astype(np.float32)
+    seeds = np.arange(n_env) + seed0
+    obs0 = np.zeros((n_env, 6), np.float32)
+    obs = np.zeros((n_env, T, 6), np.float32)
+    fobs = np.zeros((n_env, T, 6), np.float32)
+    rew = np.zeros((n_env, T))
+    done = np.zeros((n_env, T), bool)
+    init = {k: [] for k in ("state", "velocity", "position", "aux_vars", "last", "target")}
+    for e in range(n_env):
+        np.random.seed(int(seeds[e]))
+        env = cls()
+        obs0[e] = env.reset()
+        for k in init:
+            init[k].append(np.array(getattr(env, k), dtype=np.float64))
+        for t in range(T):
+            o, r, d, _ = env.step(acts[e, t])
+            fobs[e, t], rew[e, t], done[e, t] = o, float(r), bool(d)
+            if d:
+                o = env.reset()
+            obs[e, t] = o
+    np.savez_compressed(os.path.join(HERE, fname), seeds=seeds, actions=acts, obs0=obs0, obs=obs,
+                        final_obs=fobs, reward=rew, done=done,
+                        **{f"init_{k}": np.stack(v) for k, v in init.items()})
+    print(fname, "episodes ended:", int(done.sum()))
+
+
 def main():
     refharness.load_reference()
     import gym_usv.envs as E
+    if "--legacy-f64" in sys.argv:      # only the usv-asmc-ye-int-v0 / usv-pid-v0 fixtures
+        gen_legacy_f64(E, E.UsvAsmcYeIntEnv, "asmc_ye_int_traj.npz")
+        gen_legacy_f64(E, E.UsvPidEnv, "pid_traj.npz", seed0=4000)
+        return
     gen_asmc(E)
     gen_lidar(E)
     gen_traj(E, E.UsvSimpleEnv, "simple_traj.npz", 500, n_env=8, T=256)

@@ -100,3 +100,29 @@ def test_asmc_v0_trajectories_match_reference(golden):
             o.reset(idx=idx)
             np.testing.assert_array_equal(o.state[idx].astype(np.float32), g["obs"][idx, t])
     assert g["done"].sum() >= 5
+
+
+@pytest.mark.parametrize("fname,family", [("asmc_ye_int_traj.npz", "ye_int"), ("pid_traj.npz", "pid")])
+def test_legacy_f64_trajectories_match_reference(golden, fname, family):
+    """usv-asmc-ye-int-v0 (usv_asmc_ye_int_env.py:92-296) and usv-pid-v0 (usv_pid_env.py:89-276):
+    float64 state, seeded np.random resets, 2000 float32 scalar-action steps per env with resets
+    on done.  The restatement reproduces the reference's float64 arithmetic order, so obs match
+    bitwise after the float32 cast and rewards to 1 ulp-scale (the reference's np.linalg.inv /
+    BLAS matmul may round its last bit differently)."""
+    g = golden(fname)
+    n, T = g["actions"].shape
+    o = O.LegacyF64Batch(n, family)
+    obs = o.reset([int(s) for s in g["seeds"]])
+    np.testing.assert_array_equal(obs, g["obs0"])
+    for k in ("position", "target", "state"):
+        np.testing.assert_array_equal(getattr(o, k), g[f"init_{k}"])
+    for t in range(T):
+        ob, rw, dn = o.step(g["actions"][:, t])
+        np.testing.assert_array_equal(dn, g["done"][:, t], err_msg=f"t={t}")
+        np.testing.assert_allclose(ob, g["final_obs"][:, t], rtol=0, atol=1e-6, err_msg=f"t={t}")
+        np.testing.assert_allclose(rw, g["reward"][:, t], rtol=0, atol=1e-12, err_msg=f"t={t}")
+        if dn.any():
+            idx = np.flatnonzero(dn)
+            o.reset(idx=idx)
+            np.testing.assert_array_equal(o.state[idx].astype(np.float32), g["obs"][idx, t])
+    assert g["done"].sum() >= 2
