@@ -37,14 +37,19 @@ METRIC = "env-steps/sec at 65 536 parallel envs; 1/2/4/8 MI355X scaling"
 
 
 # --------------------------------------------------------------------------- byte model
+LEGACY_IDS = ("usv-asmc-v0", "usv-pid-v0", "usv-asmc-ye-int-v0")
+
+
 def algorithmic_bytes_per_env_step(env_id, mean_obs, precision="f32"):
     """Bytes one env-step must move (DESIGN.md 'Algorithmic bytes'): action in, obs/reward/flags
     out, dynamic state read+write, obstacle read (x, y, r per obstacle).  Reset traffic excluded."""
     w = 4 if precision == "f32" else 8
-    if env_id == "usv-asmc-v0":
+    if env_id in LEGACY_IDS:
         # action 4, obs 6 f32, reward, flags; state read: pose+velocity (6) + last/aux/target/
-        # action_last (19) + elapsed; write: 6 + 13 (target is read-only) + elapsed
-        return 4 + 6 * 4 + w + 2 + (25 * w + 4) + (19 * w + 4)
+        # action_last (19) + elapsed; write: 6 + 13 (target is read-only) + elapsed;
+        # usv-asmc-ye-int-v0 also reads and writes ye_int, ye_last
+        ye = 2 * w if env_id == "usv-asmc-ye-int-v0" else 0
+        return 4 + 6 * 4 + w + 2 + (25 * w + 4 + ye) + (19 * w + 4 + ye)
     act, obs, rew, flags = 8, 143 * 4, w, 2
     state_rd = 16 * w + 2 * 4          # 16 real fields + n_obs + elapsed
     state_wr = 9 * w + 2 * 4           # pose, velocity, last action, progress + elapsed, scan flag
@@ -83,8 +88,9 @@ def _cpu_worker(args):
     import numpy as np
     from oracle import usv_oracle as O
     rng = np.random.default_rng(seed)
-    if env_id == "usv-asmc-v0":
-        o = O.AsmcV0Batch(1)
+    if env_id in LEGACY_IDS:
+        o = O.AsmcV0Batch(1) if env_id == "usv-asmc-v0" else \
+            O.LegacyF64Batch(1, "pid" if env_id == "usv-pid-v0" else "ye_int")
         o.reset([seed])
 
         def one():
@@ -125,7 +131,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10000)
     ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
-    ap.add_argument("--env-id", default="usv-simple", choices=["usv-simple", "usv-asmc-simple", "usv-asmc-v0"])
+    ap.add_argument("--env-id", default="usv-simple", choices=["usv-simple", "usv-asmc-simple", *LEGACY_IDS])
     ap.add_argument("--precision", default="f32", choices=["f32", "f64"])
     ap.add_argument("--lidar", default="window", choices=["brute", "window"])
     ap.add_argument("--seed", type=int, default=0)
@@ -161,7 +167,7 @@ def main():
     gen = torch.Generator(device=dev).manual_seed(args.seed * 7919 + rank)
     if A == 2:
         lo, span = torch.tensor([0.2, -1.0], device=dev), torch.tensor([0.8, 2.0], device=dev)
-    else:                                       # usv-asmc-v0 heading offset (usv_asmc_env.py:74-75)
+    else:                                       # legacy heading offset (usv_asmc_env.py:74-75)
         lo, span = torch.tensor([-math.pi / 2], device=dev), torch.tensor([math.pi], device=dev)
     acts = torch.rand((pool, N, A), device=dev, generator=gen) * span + lo
     obs = torch.empty((N, D), device=dev)
@@ -233,7 +239,7 @@ def main():
                          "traffic": traffic, "kernel_ms": round(kern_ms, 5),
                          "algorithmic_bytes_per_env_step": round(bpe, 1)},
         }
-        if args.env_id == "usv-asmc-v0":
+        if args.env_id in LEGACY_IDS:
             out["config"].pop("lidar")
             out["config"].pop("mean_obstacles")
         if not args.no_cpu_baseline:

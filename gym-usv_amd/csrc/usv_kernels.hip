@@ -49,7 +49,8 @@ template <typename R> struct State {
   R4<R>* obst;             // [N][cap] (x, y, r, r*r)
   R* sensor_last;          // [N][128]
   R* asmc;                 // [16][N]
-  R* v0;                   // [19][fstride] usv-asmc-v0: last[9], aux[3], target[6], action_last
+  R* v0;                   // [21][fstride] legacy envs: last[9], aux[3], target[6], action_last,
+                           //   ye_int, ye_last (usv-asmc-ye-int-v0)
   const R* ray_tab;        // [128][2] (cos, sin)(start + i*res)
   R4<R>* pose;             // [N][2] pose record after the step's dynamics (split step):
                            //   (x, y, sin psi, cos psi), (partial reward, n_obs, truncated, 0)
@@ -61,7 +62,7 @@ template <typename R> struct State {
   __host__ __device__ int32_t* I(int i) const { return fint + (size_t)i * fstride; }
   __host__ __device__ R* V(int i) const { return v0 + (size_t)i * fstride; }
 };
-constexpr int kV0Last = 0, kV0Aux = 9, kV0Target = 12, kV0ALast = 18, kV0N = 19;
+constexpr int kV0Last = 0, kV0Aux = 9, kV0Target = 12, kV0ALast = 18, kV0Ye = 19, kV0N = 21;
 
 template <typename R> struct IO {
   const float* act;        // [N][2]
@@ -1433,6 +1434,7 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(State<R> S, IO<R> io) {
 constexpr double kV0MinSpeed = 0.3, kV0KAk = 5.72, kV0KYe = 0.5, kV0SigmaYe = 1.0;
 constexpr double kV0CAction = 1.0 / (((kPi / 2) / 2 - (-kPi / 2) / 2) / H * (((kPi / 2) / 2 - (-kPi / 2) / 2) / H));
 constexpr double kV0WAction = 0.2, kV0TMin = -30.0, kV0TMax = 36.5;
+constexpr int kFamV0 = 0, kFamYeInt = 1, kFamPid = 2;   // usv-asmc-v0, usv-asmc-ye-int-v0, usv-pid-v0
 
 template <typename R> __device__ __forceinline__ R q32(R x) { return R((float)x); }
 
@@ -1442,16 +1444,20 @@ __device__ __forceinline__ void v0_obs(float* row, R u, R v_ak, R r, R ye, R psi
   row[3] = (float)ye; row[4] = (float)psi_ak; row[5] = (float)a_last;
 }
 
-// UsvAsmcEnv.reset (usv_asmc_env.py:258-300); Philox draws replace np.random.uniform
-template <typename R>
+// UsvAsmcEnv.reset (usv_asmc_env.py:258-300); Philox draws replace np.random.uniform.
+// FAM 1 / 2 are the float64 legacy envs on the same template: UsvAsmcYeIntEnv.reset
+// (usv_asmc_ye_int_env.py:256-296: x, y ~ U(-5, 5), speed ~ U(0.4, 1.4)) and UsvPidEnv.reset
+// (usv_pid_env.py:236-276: speed ~ U(0.4, 1.4)); the draw order is the same in all three.
+template <typename R, int FAM = kFamV0>
 __device__ void v0_reset(const State<R>& S, int e, float* row) {
   const int ep = S.I(I_EPISODE)[e];
   Philox g(S.seed, S.gid0 + (uint64_t)e, (uint32_t)ep);
-  const double x = g.uniform(-2.5, 2.5), y = g.uniform(-2.5, 2.5);               // :260-261
+  const double lim = FAM == kFamYeInt ? 5.0 : 2.5;
+  const double x = g.uniform(-lim, lim), y = g.uniform(-lim, lim);               // :260-261
   const double psi = g.uniform(-kPi, kPi);                                        // :262
   const double x0 = g.uniform(-2.5, 2.5), y0 = g.uniform(-2.5, 2.5);             // :275-276
   const double xd = g.uniform(15.0, 30.0), yd = y0;                              // :277-278
-  const double ds = g.uniform(1.4, 2.4);                                          // :279
+  const double ds = FAM == kFamV0 ? g.uniform(1.4, 2.4) : g.uniform(0.4, 1.4);   // :279
   const double ak = (double)(float)atan2(yd - y0, xd - x0);                       // :281-282
   const double psi_ak = (double)(float)wrap_once(psi - ak);                       // :284-286
   const double ye = -(x - x0) * sin(ak) + (y - y0) * cos(ak);                     // :287
@@ -1461,6 +1467,7 @@ __device__ void v0_reset(const State<R>& S, int e, float* row) {
   const double tg[6] = {x0, y0, ds, ak, xd, yd};
   for (int i = 0; i < 6; ++i) S.V(kV0Target + i)[e] = R(tg[i]);
   S.V(kV0ALast)[e] = R(0);
+  S.V(kV0Ye)[e] = R(0); S.V(kV0Ye + 1)[e] = R(0);                                 // ye_int, ye_last
   S.I(I_ELAPSED)[e] = 0;
   S.I(I_EPISODE)[e] = ep + 1;
   v0_obs<R>(row, R(0), R(0), R(0), R(ye), R(psi_ak), R(0));                      // :289-298
@@ -1575,15 +1582,154 @@ __global__ __launch_bounds__(kBlock) void v0_step_kernel(State<R> S, IO<R> io) {
   v0_obs<R>(row, u, v_ak, r, ye, psi_ak, a);
   if (done || trunc) {
     if (io.fobs) v0_obs<R>(io.fobs + (size_t)e * 6, u, v_ak, r, ye, psi_ak, a);
-    if (S.autoreset == USV_AUTORESET_SAME_STEP) v0_reset<R>(S, e, row);
+    if (S.autoreset == USV_AUTORESET_SAME_STEP) v0_reset<R, kFamV0>(S, e, row);
   }
 }
 
-template <typename R>
+template <typename R, int FAM>
 __global__ __launch_bounds__(kBlock) void v0_reset_kernel(State<R> S, IO<R> io) {
   const int e = blockIdx.x * kBlock + threadIdx.x;
   if (e >= S.N || (io.mask && !io.mask[e])) return;
-  v0_reset<R>(S, e, io.obs + (size_t)e * 6);
+  v0_reset<R, FAM>(S, e, io.obs + (size_t)e * 6);
+}
+
+// --------------------------------------------------------------------------- float64 legacy family
+// UsvAsmcYeIntEnv (usv-asmc-ye-int-v0, usv_asmc_ye_int_env.py:92-253) and UsvPidEnv (usv-pid-v0,
+// usv_pid_env.py:89-233): the usv-asmc-v0 plant with the state kept in float64 (no float32
+// arrays), so the whole step runs in R.  Lane per env.  Statement order follows the reference
+// (contraction is off in this translation unit), so the f64 build tracks it to libm ulps.
+// Citations are usv_asmc_ye_int_env.py lines; usv_pid_env.py has the same statements 4 lines
+// earlier (its control law: :148-155).
+constexpr double kYeIntKI = 0.001;                                               // ye_int :51
+constexpr double kPidKpU = 1.1, kPidKiU = 0.2, kPidKdU = 0.1, kPidKpPsi = 0.8, kPidKdPsi = 3.0;  // pid :40-44
+constexpr double kYvK = 1.1 + 0.0045 * (1.01 / 0.09) - 0.1 * (0.27 / 0.09) + 0.016 * ((0.27 / 0.09) * (0.27 / 0.09));
+
+template <typename R, int FAM>
+__global__ __launch_bounds__(kBlock) void legacy_step_kernel(State<R> S, IO<R> io) {
+  const int e = blockIdx.x * kBlock + threadIdx.x;
+  if (e >= S.N) return;
+  const R a = R(io.act[e]);
+  R u = S.F(F_U)[e], v = S.F(F_V)[e], r = S.F(F_R)[e];
+  R x = S.F(F_X)[e], y = S.F(F_Y)[e], psi = S.F(F_PSI)[e];
+  R e_u_int = S.V(kV0Aux)[e], ka_u = S.V(kV0Aux + 1)[e], ka_psi = S.V(kV0Aux + 2)[e];
+  const R xd_l = S.V(0)[e], yd_l = S.V(1)[e], pd_l = S.V(2)[e];
+  const R ud_l = S.V(3)[e], vd_l = S.V(4)[e], rd_l = S.V(5)[e];
+  const R e_u_last = S.V(6)[e];
+  R kdu = S.V(7)[e], kdp = S.V(8)[e];
+  const R x0 = S.V(kV0Target)[e], y0 = S.V(kV0Target + 1)[e], ds = S.V(kV0Target + 2)[e];
+  const R ak = S.V(kV0Target + 3)[e];
+  const R action_dot = (a - S.V(kV0ALast)[e]) / R(H);                           // :113
+  const R psi_d = wrap_once(a + ak);                                             // :116-117
+  const bool fast = m_abs(u) > R(1.2);                                           // :119-123
+  const R xu = fast ? R(64.55) : R(-25.0), xuu = fast ? R(-70.92) : R(0.0);
+  const R mag = m_sqrt(u * u + v * v);                                           // :125-132
+  const R yv = (R(0.5) * (R(-40 * 1000) * m_abs(v))) * R(kYvK);
+  const R yr = (((R(6 * (-3.141592 * 1000)) * mag) * R(0.09)) * R(0.09)) * R(1.01);
+  const R nv = (((R(0.06 * (-3.141592 * 1000)) * mag) * R(0.09)) * R(0.09)) * R(1.01);
+  const R nr = ((((R(0.02 * (-3.141592 * 1000)) * mag) * R(0.09)) * R(0.09)) * R(1.01)) * R(1.01);
+  const R f_u = ((R(MASS - Y_V_DOT) * v * r) + (xuu * m_abs(u) + xu * u)) / R(MASS - X_U_DOT);    // :137
+  const R f_psi = ((R(-X_U_DOT + Y_V_DOT) * u * v) + (nr * r)) / R(IZ - N_R_DOT);                 // :138
+  const R e_psi = wrap_once(psi_d - psi);                                        // :140-141
+  const R e_psi_dot = R(0) - r;                                                  // :142
+  const R u_psi = R(1) / (R(1) + m_exp(R(10) * (m_abs(e_psi) * R(2 / kPi) - R(0.5))));  // :146
+  const R u_d = (ds - R(kV0MinSpeed)) * u_psi + R(kV0MinSpeed);                  // :148-149
+  const R e_u = u_d - u;                                                         // :151
+  e_u_int = R(H) * (e_u + e_u_last) / R(2) + e_u_int;                            // :152 (e_u_last stale)
+  R tx, tz;
+  if constexpr (FAM == kFamYeInt) {                                              // ASMC :154-170
+    const R sig_u = e_u + R(LAMBDA_U) * e_u_int;
+    const R sig_p = e_psi_dot + R(LAMBDA_PSI) * e_psi;
+    const R kdu_n = ka_u > R(KMIN_U) ? R(K_U) * m_sign(m_abs(sig_u) - R(MU_U)) : R(KMIN_U);
+    const R kdp_n = ka_psi > R(KMIN_PSI) ? R(K_PSI) * m_sign(m_abs(sig_p) - R(MU_PSI)) : R(KMIN_PSI);
+    ka_u = R(H) * (kdu_n + kdu) / R(2) + ka_u;
+    ka_psi = R(H) * (kdp_n + kdp) / R(2) + ka_psi;
+    kdu = kdu_n; kdp = kdp_n;
+    const R ua_u = (-ka_u * m_sqrt(m_abs(sig_u)) * m_sign(sig_u)) - R(K2_U) * sig_u;
+    const R ua_p = (-ka_psi * m_sqrt(m_abs(sig_p)) * m_sign(sig_p)) - R(K2_PSI) * sig_p;
+    tx = ((R(LAMBDA_U) * e_u) - f_u - ua_u) / R(1.0 / (MASS - X_U_DOT));
+    tz = ((R(LAMBDA_PSI) * e_psi) - f_psi - ua_p) / R(1.0 / (IZ - N_R_DOT));
+  } else {                                                                       // PID, pid :148-155
+    const R e_u_dot = (e_u - e_u_last) / R(H);
+    const R ua_u = (R(kPidKpU) * e_u) + (R(kPidKiU) * e_u_int) + (R(kPidKdU) * e_u_dot);
+    const R ua_p = (R(kPidKpPsi) * e_psi) + (R(kPidKdPsi) * e_psi_dot);
+    tx = (-f_u + ua_u) / R(1.0 / (MASS - X_U_DOT));
+    tz = (-f_psi + ua_p) / R(1.0 / (IZ - N_R_DOT));
+  }
+  R tport = tx / R(2) + tz / R(B_TH);                                            // :172-178
+  R tstbd = tx / R(2 * C_TH) - tz / R(B_TH * C_TH);
+  tport = tport > R(kV0TMax) ? R(kV0TMax) : tport;
+  tport = tport < R(kV0TMin) ? R(kV0TMin) : tport;
+  tstbd = tstbd > R(kV0TMax) ? R(kV0TMax) : tstbd;
+  tstbd = tstbd < R(kV0TMin) ? R(kV0TMin) : tstbd;
+  const R t0 = tport + R(C_TH) * tstbd;                                          // :184
+  const R t2 = R(0.5 * B_TH) * (tport - R(C_TH) * tstbd);
+  // C = CRB + CA, D = Dl - Dn (:186-205): their non-zero entries
+  const R c02 = (R(0) - R(MASS) * v) + R(2) * ((R(Y_V_DOT) * v) + R((Y_R_DOT + N_V_DOT) / 2) * r);
+  const R c12 = (R(MASS) * u) + (R(0) - R(X_U_DOT * MASS) * u);
+  const R c20 = (R(MASS) * v) + R(2) * ((R(0 - Y_V_DOT) * v) - R((Y_R_DOT + N_V_DOT) / 2) * r);
+  const R c21 = (R(0) - R(MASS) * u) + (R(X_U_DOT * MASS) * u);
+  const R av = m_abs(v), ar = m_abs(r);
+  const R d00 = (R(0) - xu) - xuu * m_abs(u);
+  const R d11 = (R(0) - yv) - (R(YVV) * av + R(YVR) * ar);
+  const R d12 = (R(0) - yr) - (R(YRV) * av + R(YRR) * ar);
+  const R d21 = (R(0) - nv) - (R(NVV) * av + R(NVR) * ar);
+  const R d22 = (R(0) - nr) - (R(NRV) * av + R(NRR) * ar);
+  const R rhs0 = (t0 - c02 * r) - d00 * u;                                       // :207-208
+  const R rhs1 = (R(0) - c12 * r) - (d11 * v + d12 * r);
+  const R rhs2 = (t2 - (c20 * u + c21 * v)) - (d21 * v + d22 * r);
+  const R ud = R(MI00) * rhs0;                                                   // M^-1 (block form)
+  const R vd = R(MI11) * rhs1 + R(MI12) * rhs2;
+  const R rd = R(MI21) * rhs1 + R(MI22) * rhs2;
+  u = R(H) * (ud + ud_l) / R(2) + u;                                             // :209-211
+  v = R(H) * (vd + vd_l) / R(2) + v;
+  r = R(H) * (rd + rd_l) / R(2) + r;
+  const R cj = m_cos(psi), sj = m_sin(psi);                                      // J(psi) :213-215
+  const R xd = cj * u - sj * v, yd = sj * u + cj * v, pd = r;
+  x = R(H) * (xd + xd_l) / R(2) + x;                                             // :217-219
+  y = R(H) * (yd + yd_l) / R(2) + y;
+  psi = wrap_once(R(H) * (pd + pd_l) / R(2) + psi);                              // :221-222
+  const R psi_ak = wrap_once(psi - ak);                                          // :224-225
+  const R ye = -(x - x0) * m_sin(ak) + (y - y0) * m_cos(ak);                     // :227
+  const R ye_abs = m_abs(ye);
+  const R pa = m_abs(psi_ak);
+  const R r_act = R(kV0WAction) * tanh(R(-kV0CAction) * (action_dot * action_dot));
+  const R r_ak = -m_exp(R(kV0KAk) * (pa - R(kPi)));
+  R ye_obs = ye, reward;
+  if constexpr (FAM == kFamYeInt) {
+    R ye_int = S.V(kV0Ye)[e];
+    const R ye_last = S.V(kV0Ye + 1)[e];
+    if (m_sign(ye) != m_sign(ye_last)) ye_int = R(0);                            // :230-231
+    ye_int = R(H) * (ye + ye_last) + ye_int;                                     // :232
+    ye_obs = ye + R(kYeIntKI) * ye_int;                                          // ye_ss :235
+    S.V(kV0Ye)[e] = ye_int;
+    S.V(kV0Ye + 1)[e] = ye;
+    reward = r_act + (pa < R(kPi / 2) ? m_exp(R(-kV0KYe) * ye_abs) : r_ak);      // :350-360
+  } else {
+    const R r_ye = ye_abs > R(kV0SigmaYe) ? m_exp(R(-kV0KYe) * ye_abs)
+                                          : m_exp(R(-kV0KYe) * (ye_abs * ye_abs) / R(kV0SigmaYe));
+    reward = pa < R(kPi / 2) ? r_act + r_ye : r_ak;                              // pid :329-338
+  }
+  const R v_ak = m_sin(psi_ak) * u + m_cos(psi_ak) * v;                          // body_to_path :239
+  const bool done = ye_abs > R(10) || x < R(-10);                                // :241-245
+  const int el = S.I(I_ELAPSED)[e] + 1;
+  const bool trunc = !done && S.limit > 0 && el >= S.limit;
+  io.rew[e] = done ? R(-1) : reward;
+  io.term[e] = done;
+  io.trunc[e] = trunc;
+  S.F(F_U)[e] = u; S.F(F_V)[e] = v; S.F(F_R)[e] = r;                             // :247-251
+  S.F(F_X)[e] = x; S.F(F_Y)[e] = y; S.F(F_PSI)[e] = psi;
+  S.V(kV0Aux)[e] = e_u_int; S.V(kV0Aux + 1)[e] = ka_u; S.V(kV0Aux + 2)[e] = ka_psi;
+  S.V(0)[e] = xd; S.V(1)[e] = yd; S.V(2)[e] = pd;
+  S.V(3)[e] = ud; S.V(4)[e] = vd; S.V(5)[e] = rd;
+  S.V(7)[e] = kdu; S.V(8)[e] = kdp;
+  S.V(kV0ALast)[e] = a;
+  S.I(I_ELAPSED)[e] = el;
+  float* row = io.obs + (size_t)e * 6;
+  v0_obs<R>(row, u, v_ak, r, ye_obs, psi_ak, a);
+  if (done || trunc) {
+    if (io.fobs) v0_obs<R>(io.fobs + (size_t)e * 6, u, v_ak, r, ye_obs, psi_ak, a);
+    if (S.autoreset == USV_AUTORESET_SAME_STEP) v0_reset<R, FAM>(S, e, row);
+  }
 }
 
 }  // namespace usv
@@ -1613,7 +1759,11 @@ const FieldDesc kFields[USV_FIELD_COUNT] = {
     {"progress", 0}, {"path_x0", 0}, {"path_y0", 0}, {"path_x1", 0}, {"path_y1", 0},
     {"max_u", 0}, {"max_r", 0}, {"ref_v", 0}, {"n_obs", 1}, {"elapsed", 1}, {"episode", 1},
     {"scan_valid", 1}, {"obs_x", 0}, {"obs_y", 0}, {"obs_r", 0}, {"sensor_last", 0}, {"asmc", 0},
-    {"v0_last", 0}, {"v0_aux", 0}, {"v0_target", 0}, {"v0_action_last", 0}};
+    {"v0_last", 0}, {"v0_aux", 0}, {"v0_target", 0}, {"v0_action_last", 0}, {"v0_ye", 0}};
+
+bool is_legacy(int mode) {   // lane-per-env legacy envs: obs 6, scalar action, no lidar
+  return mode == USV_MODE_ASMC_V0 || mode == USV_MODE_ASMC_YE_INT_V0 || mode == USV_MODE_PID_V0;
+}
 
 struct Handle {
   usv_config cfg;
@@ -1773,8 +1923,14 @@ template <typename R>
 int launch_step(Handle* h, State<R>& S, const float* act, float* obs, void* rew, uint8_t* term,
                 uint8_t* trunc, float* fobs, hipStream_t st) {
   IO<R> io{act, obs, (R*)rew, term, trunc, fobs, nullptr};
-  if (h->cfg.mode == USV_MODE_ASMC_V0) {
-    hipLaunchKernelGGL((v0_step_kernel<R>), dim3((S.N + kBlock - 1) / kBlock), dim3(kBlock), 0, st, S, io);
+  if (is_legacy(h->cfg.mode)) {
+    const dim3 grid((S.N + kBlock - 1) / kBlock), block(kBlock);
+    if (h->cfg.mode == USV_MODE_ASMC_V0)
+      hipLaunchKernelGGL((v0_step_kernel<R>), grid, block, 0, st, S, io);
+    else if (h->cfg.mode == USV_MODE_ASMC_YE_INT_V0)
+      hipLaunchKernelGGL((legacy_step_kernel<R, kFamYeInt>), grid, block, 0, st, S, io);
+    else
+      hipLaunchKernelGGL((legacy_step_kernel<R, kFamPid>), grid, block, 0, st, S, io);
     HIP_TRY(hipGetLastError());
     return USV_OK;
   }
@@ -1830,8 +1986,13 @@ template <typename R>
 int launch_reset(Handle* h, State<R>& S, const uint8_t* mask, float* obs, hipStream_t st) {
   IO<R> io{nullptr, obs, nullptr, nullptr, nullptr, nullptr, mask};
   const dim3 grid((S.N + kEPBReset - 1) / kEPBReset), block(kBlock);
+  const dim3 lgrid((S.N + kBlock - 1) / kBlock);
   if (h->cfg.mode == USV_MODE_ASMC_V0)
-    hipLaunchKernelGGL((v0_reset_kernel<R>), dim3((S.N + kBlock - 1) / kBlock), dim3(kBlock), 0, st, S, io);
+    hipLaunchKernelGGL((v0_reset_kernel<R, kFamV0>), lgrid, block, 0, st, S, io);
+  else if (h->cfg.mode == USV_MODE_ASMC_YE_INT_V0)
+    hipLaunchKernelGGL((v0_reset_kernel<R, kFamYeInt>), lgrid, block, 0, st, S, io);
+  else if (h->cfg.mode == USV_MODE_PID_V0)
+    hipLaunchKernelGGL((v0_reset_kernel<R, kFamPid>), lgrid, block, 0, st, S, io);
   else if (h->cfg.mode == USV_MODE_SIMPLE)
     hipLaunchKernelGGL((reset_kernel<R, USV_MODE_SIMPLE>), grid, block, lds_head_bytes<R>() + kWaves * 3 * 64 * sizeof(R), st, S, io);
   else
@@ -1847,13 +2008,14 @@ int field_per_env(const Handle* h, int f) {
   if (f == USV_FIELD_V0_LAST) return 9;
   if (f == USV_FIELD_V0_AUX) return 3;
   if (f == USV_FIELD_V0_TARGET) return 6;
+  if (f == USV_FIELD_V0_YE) return 2;
   return 1;
 }
 
 // first v0 SoA row of a v0 field
 int v0_base(int f) {
   return f == USV_FIELD_V0_LAST ? kV0Last : f == USV_FIELD_V0_AUX ? kV0Aux
-       : f == USV_FIELD_V0_TARGET ? kV0Target : kV0ALast;
+       : f == USV_FIELD_V0_TARGET ? kV0Target : f == USV_FIELD_V0_YE ? kV0Ye : kV0ALast;
 }
 
 // host <-> device for one field; host side [N][per] float64 / int32
@@ -1928,7 +2090,7 @@ int field_io(Handle* h, State<R>& S, int f, void* host, bool to_host) {
     }
     return USV_OK;
   }
-  if (f >= USV_FIELD_V0_LAST && f <= USV_FIELD_V0_ACTION_LAST) {   // device SoA rows, host [N][per]
+  if (f >= USV_FIELD_V0_LAST && f <= USV_FIELD_V0_YE) {   // device SoA rows, host [N][per]
     const int per = field_per_env(h, f), base = v0_base(f);
     std::vector<R> tmp(N);
     double* hd = (double*)host;
@@ -1983,7 +2145,7 @@ void usv_config_default(usv_config* cfg, int32_t mode, int32_t num_envs) {
   cfg->precision = USV_F32;
   cfg->num_envs = num_envs;
   cfg->obstacle_cap = 32;
-  cfg->max_episode_steps = mode == USV_MODE_ASMC_SIMPLE ? 1000 : mode == USV_MODE_ASMC_V0 ? 0 : 500;  // gym_usv/__init__.py
+  cfg->max_episode_steps = mode == USV_MODE_ASMC_SIMPLE ? 1000 : is_legacy(mode) ? 0 : 500;  // gym_usv/__init__.py
   cfg->autoreset = USV_AUTORESET_SAME_STEP;
   cfg->lidar_algo = USV_LIDAR_WINDOW;
   cfg->seed = 0;
@@ -1994,7 +2156,7 @@ int usv_create(const usv_config* cfg, int32_t device, void** out) {
   if (!cfg || !out) return fail(USV_ERR_ARG, "null argument");
   *out = nullptr;
   if (cfg->abi_version != USV_ABI_VERSION) return fail(USV_ERR_ABI, "abi_version mismatch");
-  if (cfg->mode != USV_MODE_SIMPLE && cfg->mode != USV_MODE_ASMC_SIMPLE && cfg->mode != USV_MODE_ASMC_V0)
+  if (cfg->mode != USV_MODE_SIMPLE && cfg->mode != USV_MODE_ASMC_SIMPLE && !is_legacy(cfg->mode))
     return fail(USV_ERR_ARG, "unknown mode");
   if (cfg->precision != USV_F32 && cfg->precision != USV_F64)
     return fail(USV_ERR_ARG, "unknown precision");
@@ -2064,10 +2226,10 @@ void usv_destroy(void* hp) {
 
 int usv_num_envs(void* hp) { return hp ? as_handle(hp)->cfg.num_envs : fail(USV_ERR_ARG, "null handle"); }
 int usv_obs_dim(void* hp) {
-  return hp ? (as_handle(hp)->cfg.mode == USV_MODE_ASMC_V0 ? 6 : kObsDim) : fail(USV_ERR_ARG, "null handle");
+  return hp ? (is_legacy(as_handle(hp)->cfg.mode) ? 6 : kObsDim) : fail(USV_ERR_ARG, "null handle");
 }
 int usv_act_dim(void* hp) {
-  return hp ? (as_handle(hp)->cfg.mode == USV_MODE_ASMC_V0 ? 1 : 2) : fail(USV_ERR_ARG, "null handle");
+  return hp ? (is_legacy(as_handle(hp)->cfg.mode) ? 1 : 2) : fail(USV_ERR_ARG, "null handle");
 }
 int usv_reward_bytes(void* hp) {
   return hp ? (as_handle(hp)->cfg.precision == USV_F64 ? 8 : 4) : fail(USV_ERR_ARG, "null handle");

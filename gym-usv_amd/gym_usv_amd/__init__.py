@@ -5,6 +5,8 @@ Registry mirroring gym_usv/__init__.py:3-39 for the ids on the accelerated path:
     make("usv-simple")                         -> UsvSimpleEnv with TimeLimit(500)
     make("usv-asmc-simple")                    -> UsvSimpleASMCEnv with TimeLimit(1000)
     make("usv-asmc-v0")                        -> legacy UsvAsmcEnv (old gym API, no TimeLimit)
+    make("usv-pid-v0")                         -> legacy UsvPidEnv (float64 PID plant)
+    make("usv-asmc-ye-int-v0")                 -> legacy UsvAsmcYeIntEnv (float64, ye integral)
     make_vec("usv-simple", num_envs=65536)     -> UsvVectorEnv (one HIP launch per step)
     make_sb3_vec_env("usv-simple", 4096, 5)    -> SB3 VecEnv (NumPy out, Monitor infos, VecFrameStack(5))
 
@@ -16,13 +18,15 @@ from .vector_env import ENV_SPECS, UsvVectorEnv  # noqa: F401
 __all__ = ["make", "make_vec", "make_sb3_vec_env", "registry", "UsvVectorEnv", "UsvLibError", "ENV_SPECS"]
 
 registry = {k: {"entry_point": f"gym_usv_amd.envs:{cls}", "max_episode_steps": v[1] or None}
-            for (k, v), cls in zip(ENV_SPECS.items(), ("UsvSimpleEnv", "UsvSimpleASMCEnv", "UsvAsmcEnv"))}
+            for (k, v), cls in zip(ENV_SPECS.items(), ("UsvSimpleEnv", "UsvSimpleASMCEnv", "UsvAsmcEnv",
+                                                       "UsvPidEnv", "UsvAsmcYeIntEnv"))}
 
 
 def make(env_id, max_episode_steps=None, **kwargs):
     from . import envs
     cls = {"usv-simple": envs.UsvSimpleEnv, "usv-asmc-simple": envs.UsvSimpleASMCEnv,
-           "usv-asmc-v0": envs.UsvAsmcEnv}[env_id]
+           "usv-asmc-v0": envs.UsvAsmcEnv, "usv-pid-v0": envs.UsvPidEnv,
+           "usv-asmc-ye-int-v0": envs.UsvAsmcYeIntEnv}[env_id]
     limit = registry[env_id]["max_episode_steps"] if max_episode_steps is None else max_episode_steps
     limit = limit or 0
     return cls(max_episode_steps=limit, **kwargs)

@@ -15,7 +15,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 LIB_PATH = os.environ.get("USV_LIB_PATH", LIB_PATH)
 
 ABI_VERSION = 1
-MODE_SIMPLE, MODE_ASMC_SIMPLE, MODE_ASMC_V0 = 0, 1, 2
+MODE_SIMPLE, MODE_ASMC_SIMPLE, MODE_ASMC_V0, MODE_ASMC_YE_INT_V0, MODE_PID_V0 = 0, 1, 2, 3, 4
 F32, F64 = 0, 1
 AUTORESET_SAME_STEP, AUTORESET_DISABLED = 0, 1
 LIDAR_BRUTE, LIDAR_WINDOW = 0, 1

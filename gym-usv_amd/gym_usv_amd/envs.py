@@ -73,3 +73,14 @@ class UsvAsmcEnv(_SingleEnv):
     def step(self, action):
         obs, r, term, trunc, info = super().step(action)
         return obs, r, term or trunc, info
+
+
+class UsvPidEnv(UsvAsmcEnv):
+    """HIP-backed legacy ``UsvPidEnv`` (id usv-pid-v0, usv_pid_env.py:14), old gym API."""
+    env_id = "usv-pid-v0"
+
+
+class UsvAsmcYeIntEnv(UsvAsmcEnv):
+    """HIP-backed legacy ``UsvAsmcYeIntEnv`` (id usv-asmc-ye-int-v0, usv_asmc_ye_int_env.py:14),
+    old gym API."""
+    env_id = "usv-asmc-ye-int-v0"

@@ -22,12 +22,15 @@ ENV_SPECS = {
     "usv-simple": (_lib.MODE_SIMPLE, 500),
     "usv-asmc-simple": (_lib.MODE_ASMC_SIMPLE, 1000),
     "usv-asmc-v0": (_lib.MODE_ASMC_V0, 0),      # registered without max_episode_steps (:3-6)
+    "usv-pid-v0": (_lib.MODE_PID_V0, 0),        # :8-11
+    "usv-asmc-ye-int-v0": (_lib.MODE_ASMC_YE_INT_V0, 0),   # :13-16
 }
+LEGACY_IDS = ("usv-asmc-v0", "usv-pid-v0", "usv-asmc-ye-int-v0")
 
 
 def _spaces(env_id):
     """Observation / action spaces as the reference declares them."""
-    if env_id == "usv-asmc-v0":                  # usv_asmc_env.py:74-96
+    if env_id in LEGACY_IDS:    # usv_asmc_env.py:74-96, usv_pid_env.py:75-86, usv_asmc_ye_int_env.py:80-90
         lo = np.array([-1.5, -1.5, -1.0, -10, -np.pi, -np.pi / 2], dtype=np.float32)
         hi = np.array([1.5, 1.5, 1.0, 10, np.pi, np.pi / 2], dtype=np.float32)
         return (Box(lo, hi, dtype=np.float32),

@@ -12,13 +12,17 @@
  *   usv_seed        <- Env.reset(seed=...) seeding of np_random (simple_env.py:229)
  *   usv_reset       <- UsvSimpleEnv.reset (simple_env.py:228-308),
  *                      UsvSimpleASMCEnv.reset (simple_env_asmc.py:14-16),
- *                      UsvAsmcEnv.reset (usv_asmc_env.py:258-300)
+ *                      UsvAsmcEnv.reset (usv_asmc_env.py:258-300),
+ *                      UsvAsmcYeIntEnv.reset (usv_asmc_ye_int_env.py:256-296),
+ *                      UsvPidEnv.reset (usv_pid_env.py:236-276)
  *   usv_step        <- UsvSimpleEnv.step (simple_env.py:310-346),
  *                      UsvSimpleASMCEnv.step (simple_env_asmc.py:18-27) -> UsvAsmc.compute
  *                      (gym_usv/control/usv_asmc.py:53-244), lidar
  *                      (gym_usv/envs/usv_asmc_ca_env.py:411-461,500-519), TimeLimit
  *                      (gym_usv/__init__.py:27,33) and DummyVecEnv same-step autoreset;
- *                      legacy UsvAsmcEnv.step (usv_asmc_env.py:99-255, compute_reward :364-374)
+ *                      legacy UsvAsmcEnv.step (usv_asmc_env.py:99-255, compute_reward :364-374),
+ *                      UsvAsmcYeIntEnv.step (usv_asmc_ye_int_env.py:92-253, :350-360),
+ *                      UsvPidEnv.step (usv_pid_env.py:89-233, :329-338)
  *   usv_get_field / usv_set_field / usv_get_state / usv_set_state
  *                   <- the env attributes (position, velocity, obstacle_positions, ...);
  *                      used for checkpointing and for parity state injection
@@ -57,8 +61,11 @@ typedef enum usv_status {
 typedef enum usv_mode {
   USV_MODE_SIMPLE = 0,       /* id "usv-simple"      (UsvSimpleEnv)                      */
   USV_MODE_ASMC_SIMPLE = 1,  /* id "usv-asmc-simple" (UsvSimpleASMCEnv)                  */
-  USV_MODE_ASMC_V0 = 2       /* id "usv-asmc-v0" legacy UsvAsmcEnv (usv_asmc_env.py:14): */
+  USV_MODE_ASMC_V0 = 2,      /* id "usv-asmc-v0" legacy UsvAsmcEnv (usv_asmc_env.py:14): */
                              /* obs 6, scalar action, no lidar, no TimeLimit             */
+  USV_MODE_ASMC_YE_INT_V0 = 3, /* id "usv-asmc-ye-int-v0" UsvAsmcYeIntEnv               */
+                               /* (usv_asmc_ye_int_env.py:14): float64, ye integral      */
+  USV_MODE_PID_V0 = 4          /* id "usv-pid-v0" UsvPidEnv (usv_pid_env.py:14): float64 */
 } usv_mode;
 
 typedef enum usv_precision { USV_F32 = 0, USV_F64 = 1 } usv_precision;
@@ -108,6 +115,7 @@ typedef enum usv_field {
   USV_FIELD_V0_AUX,         /* [3]  usv-asmc-v0 `aux_vars` (e_u_int, Ka_u, Ka_psi)        */
   USV_FIELD_V0_TARGET,      /* [6]  usv-asmc-v0 `target` (x_0, y_0, speed, ak, x_d, y_d)  */
   USV_FIELD_V0_ACTION_LAST, /* [1]  usv-asmc-v0 state[5] (previous action)                 */
+  USV_FIELD_V0_YE,          /* [2]  usv-asmc-ye-int-v0 aux_vars[3] ye_int, last[9] ye_last  */
   USV_FIELD_COUNT
 } usv_field;
 
@@ -115,15 +123,15 @@ int usv_abi_version(void);
 const char* usv_last_error(void);
 
 /* Fill `cfg` with the reference defaults for `mode` (cap 32, TimeLimit by id -- 500, 1000,
- * none for usv-asmc-v0 --, f32, same-step autoreset, window lidar, seed 0). */
+ * none for the legacy *-v0 ids --, f32, same-step autoreset, window lidar, seed 0). */
 void usv_config_default(usv_config* cfg, int32_t mode, int32_t num_envs);
 
 int usv_create(const usv_config* cfg, int32_t device, void** handle_out);
 void usv_destroy(void* handle);
 
 int usv_num_envs(void* handle);
-int usv_obs_dim(void* handle);   /* 143 (usv-simple, usv-asmc-simple) or 6 (usv-asmc-v0) */
-int usv_act_dim(void* handle);   /* 2, or 1 for usv-asmc-v0 */
+int usv_obs_dim(void* handle);   /* 143 (usv-simple, usv-asmc-simple) or 6 (legacy *-v0 ids) */
+int usv_act_dim(void* handle);   /* 2, or 1 for the legacy *-v0 ids */
 /* Bytes of one reward element (4 for USV_F32, 8 for USV_F64). */
 int usv_reward_bytes(void* handle);
 
@@ -137,7 +145,7 @@ int usv_reset(void* handle, const uint8_t* mask_dev, float* obs_dev, void* strea
 
 /* One env step for every env.
  *   act_dev       [num_envs][act_dim] f32 (u in [0.2,1], r in [-1,1]; usv-asmc-simple: (u_d, psi
- *                 offset); usv-asmc-v0: heading offset in [-pi/2, pi/2])
+ *                 offset); legacy *-v0 ids: heading offset in [-pi/2, pi/2])
  *   obs_dev       [num_envs][obs_dim] f32  (reset obs for envs that autoreset)
  *   rew_dev       [num_envs] f32 or f64 (usv_reward_bytes)
  *   term_dev, trunc_dev [num_envs] u8

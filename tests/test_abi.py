@@ -45,6 +45,9 @@ def test_abi_version_and_defaults(lib):
     assert (cfg.abi_version, cfg.num_envs, cfg.obstacle_cap, cfg.max_episode_steps) == (1, 128, 32, 500)
     lib.usv_config_default(ctypes.byref(cfg), _lib.MODE_ASMC_SIMPLE, 8)
     assert cfg.max_episode_steps == 1000          # gym_usv/__init__.py:33
+    for mode in (_lib.MODE_ASMC_V0, _lib.MODE_PID_V0, _lib.MODE_ASMC_YE_INT_V0):
+        lib.usv_config_default(ctypes.byref(cfg), mode, 8)
+        assert cfg.max_episode_steps == 0         # registered without a TimeLimit (:3-16)
 
 
 def test_create_rejects_bad_config_without_gpu(lib):
@@ -56,6 +59,10 @@ def test_create_rejects_bad_config_without_gpu(lib):
     assert lib.usv_create(ctypes.byref(cfg), 0, ctypes.byref(h)) != 0
     assert b"obstacle_cap" in lib.usv_last_error()
     cfg.obstacle_cap = 32
+    cfg.mode = 5                                   # no such id
+    assert lib.usv_create(ctypes.byref(cfg), 0, ctypes.byref(h)) == -1
+    assert b"mode" in lib.usv_last_error()
+    cfg.mode = _lib.MODE_SIMPLE
     cfg.abi_version = 99
     assert lib.usv_create(ctypes.byref(cfg), 0, ctypes.byref(h)) == -3
     assert not h.value

@@ -508,3 +508,111 @@ def test_v0_reset_distribution():
         assert p > 1e-4, name
     assert np.all(tg[:, 3] == 0) and np.all(obs[:, [0, 1, 2, 5]] == 0)     # ak == 0 (y_d = y_0)
     env.close()
+
+
+# --------------------------------------------------------------------------- usv-asmc-ye-int-v0 / usv-pid-v0
+LEGACY_F64 = [("usv-asmc-ye-int-v0", "ye_int", "asmc_ye_int_traj.npz"), ("usv-pid-v0", "pid", "pid_traj.npz")]
+
+
+def _legacy_inject(env, o):
+    env.set_state({"x": o.position[:, 0], "y": o.position[:, 1], "psi": o.position[:, 2],
+                   "u": o.velocity[:, 0], "v": o.velocity[:, 1], "r": o.velocity[:, 2],
+                   "v0_last": o.last[:, :9], "v0_aux": o.aux[:, :3], "v0_target": o.target,
+                   "v0_action_last": o.state[:, 5],
+                   "v0_ye": np.stack([o.aux[:, 3], o.last[:, 9]], axis=1), "elapsed": 0})
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+@pytest.mark.parametrize("env_id,family,fname", LEGACY_F64)
+def test_legacy_f64_golden_trajectory_replay(golden, env_id, family, fname, precision):
+    """Reference usv-asmc-ye-int-v0 / usv-pid-v0 rollouts (usv_asmc_ye_int_env.py:92-253,
+    usv_pid_env.py:89-233) replayed from the reference's reset state, autoreset off, up to each
+    env's first done.  f64: the kernel follows the reference's float64 statement order, so only
+    libm ulps separate them (obs to 1e-6 over 2000 steps); f32: 600 steps at 2e-3."""
+    g = golden(fname)
+    n, T = g["actions"].shape
+    env = make(env_id, n, precision=precision, autoreset=False)
+    o = O.LegacyF64Batch(n, family)
+    o.reset([int(s) for s in g["seeds"]])
+    _legacy_inject(env, o)
+    alive = np.ones(n, bool)
+    worst_o = worst_r = 0.0
+    tol_o, tol_r = (1e-6, 1e-8) if precision == "f64" else (2e-3, 2e-3)
+    steps = T if precision == "f64" else 600
+    for t in range(steps):
+        obs, rew, term, trunc, _ = env.step(torch.from_numpy(g["actions"][:, t:t + 1]).cuda())
+        obs, rew, term = to_np(obs, rew, term)
+        m = alive
+        if not m.any():
+            break
+        worst_o = max(worst_o, float(np.abs(obs[m] - g["final_obs"][m, t]).max()))
+        worst_r = max(worst_r, float(np.abs(rew[m] - g["reward"][m, t]).max()))
+        np.testing.assert_array_equal(term[m], g["done"][m, t], err_msg=f"t={t}")
+        alive = alive & ~g["done"][:, t]
+    print(f"\n[golden {env_id} {precision}] max |obs| err {worst_o:.3e}, max |rew| err {worst_r:.3e}")
+    assert worst_o <= tol_o and worst_r <= tol_r
+    env.close()
+
+
+@pytest.mark.parametrize("precision", ["f32", "f64"])
+@pytest.mark.parametrize("env_id,family,fname", LEGACY_F64)
+def test_legacy_f64_single_step_parity_4096(env_id, family, fname, precision):
+    """4096 envs scattered by 60 oracle steps (with resets), state injected, three steps with
+    same-step autoreset; terminal rows come from final_obs."""
+    n = 4096
+    o = O.LegacyF64Batch(n, family)
+    o.reset(list(range(n)))
+    rng = np.random.default_rng(4)
+    bias = np.where(np.arange(n) % 2 == 0, 1.3, -1.3)          # drive half the envs off the path
+    for _ in range(60):
+        _, _, dn = o.step(np.clip(bias + rng.normal(0, 0.3, n), -np.pi / 2, np.pi / 2).astype(np.float32))
+        if dn.any():
+            o.reset(idx=np.flatnonzero(dn))
+    # every 8th env a few mm inside |ye| = 10 (ak = 0, so ye = y - y_0): episodes end in-kernel
+    edge = np.arange(0, n, 8)
+    o.target[edge, 1] = o.position[edge, 1] - np.where(edge % 16 == 0, 9.997, -9.997)
+    env = make(env_id, n, precision=precision, autoreset=True)
+    dones = 0
+    for k in range(3):
+        _legacy_inject(env, o)
+        a = rng.uniform(-np.pi / 2, np.pi / 2, n).astype(np.float32)
+        obs, rew, term, trunc, info = env.step(torch.from_numpy(a).cuda())
+        g_obs, g_rew, g_term, g_fobs = to_np(obs, rew, term, info["final_obs"])
+        o_obs, o_rew, o_done = o.step(a)
+        assert (g_term != o_done).sum() <= 1
+        ok = g_term == o_done
+        rows = np.where((g_term & ok)[:, None], g_fobs, g_obs)
+        tol = 1e-6 if precision == "f64" else 2e-4
+        err = np.abs(rows[ok] - o_obs[ok])
+        rerr = np.abs(g_rew[ok] - o_rew[ok]).max()
+        print(f"[{env_id} {precision} round {k}] obs max err {err.max():.3e}, reward max err "
+              f"{rerr:.3e}, done {int(o_done.sum())}")
+        assert err.max() <= tol
+        assert rerr <= (1e-9 if precision == "f64" else 1e-3)
+        dones += int(o_done.sum())
+        if o_done.any():
+            o.reset(idx=np.flatnonzero(o_done))
+    assert dones > 0
+    env.close()
+
+
+@pytest.mark.parametrize("env_id,family,fname", LEGACY_F64)
+def test_legacy_f64_reset_distribution(env_id, family, fname):
+    from scipy import stats
+    n = 8192
+    env = make(env_id, n, seed=6)
+    obs, _ = env.reset(seed=6)
+    (obs,) = to_np(obs)
+    g = env.get_state()
+    o = O.LegacyF64Batch(n, family)
+    o_obs = o.reset(list(range(n)))
+    tg = g["v0_target"]
+    for name, a, b in (("x", g["x"], o.position[:, 0]), ("y", g["y"], o.position[:, 1]),
+                       ("psi", g["psi"], o.position[:, 2]), ("x0", tg[:, 0], o.target[:, 0]),
+                       ("speed", tg[:, 2], o.target[:, 2]), ("x_d", tg[:, 4], o.target[:, 4]),
+                       ("ye", obs[:, 3], o_obs[:, 3])):
+        p = stats.ks_2samp(a, b).pvalue
+        print(f"KS {env_id} {name}: p={p:.3g}")
+        assert p > 1e-4, name
+    assert np.all(g["v0_ye"] == 0) and np.all(obs[:, [0, 1, 2, 5]] == 0)
+    env.close()
