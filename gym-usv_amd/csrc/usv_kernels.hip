@@ -1323,7 +1323,12 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
         dma_copy(S.obst + (size_t)(eb + 2 * nxt) * cap, nbuf, min(2, nbe - 2 * nxt) * rowb);
       }
       Scan<float> sa, sb;
+#ifdef USV_ABL_NOLIDAR   // diagnostic ablation only: readings from the row, no scan
+      sa.rd0 = sb.rd0 = reinterpret_cast<const float4*>(cbuf)[l & 31].x + PP.pxA;
+      sa.rd1 = sb.rd1 = PP.pyB; sa.term = sb.term = false; sa.far = sb.far = false;
+#else
       lidar_wave2(reinterpret_cast<float4*>(cbuf), cap, nA, nB, PP, L.rayoff, L.slot, L.mark, sa, sb);
+#endif
       unsigned term_m = 0, coll_m = 0;
       const int nb = hasB ? 2 : 1;
       for (int k = 0; k < nb; ++k)
