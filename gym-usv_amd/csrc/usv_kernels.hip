@@ -2182,10 +2182,13 @@ int usv_create(const usv_config* cfg, int32_t device, void** out) {
   h->lid = cfg->lidar_algo == USV_LIDAR_BRUTE ? (kLidSkip | kLidUnroll2) : (kLidSkip | kLidUnroll2 | kLidWindow);
   // tuned defaults at 65 536 envs on MI355X (tools/sweep_variants.py, profiles/): usv-simple
   // (f32, window lidar) runs the fused block-queue step, else the fused wave kernel at 16
-  // envs/wave; usv-asmc-simple the split step (its 20-substep dynamics want full 64-lane waves)
-  // at 4 envs/wave
-  if (cfg->mode == USV_MODE_ASMC_SIMPLE) { h->kind = 2; h->epb = 16; }
-  else if (cfg->precision == USV_F32 && cfg->lidar_algo == USV_LIDAR_WINDOW && cfg->obstacle_cap <= 32) {
+  // envs/wave; usv-asmc-simple the split block-queue step, else the split wave scan at 4 envs/wave
+  const bool queue = cfg->precision == USV_F32 && cfg->lidar_algo == USV_LIDAR_WINDOW && cfg->obstacle_cap <= 32;
+  if (cfg->mode == USV_MODE_ASMC_SIMPLE) {
+    // ASMC's 20 substeps want full-width dynamics: a separate dyn_kernel, then the block queue
+    // (45.7 us vs 46.7 for the split wave scan at 65 536 envs)
+    if (queue) { h->kind = 4; h->epb = 128; } else { h->kind = 2; h->epb = 16; }
+  } else if (queue) {
     h->kind = 5; h->epb = 128;          // block-queue step, 16-wave blocks
   } else { h->kind = 1; h->epb = 64; }
   if (const char* v = std::getenv("USV_STEP_VARIANT")) {   // "epb,lid[,kind]" tuning override
