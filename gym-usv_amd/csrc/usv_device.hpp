@@ -11,6 +11,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 // No implicit a*b+c contraction anywhere in the device code: every fused multiply-add is an
 // explicit m_fma/fmaf.  With contraction left to the backend, the same inlined function can
 // round differently in different kernels (it depends on the surrounding code), and the step
@@ -89,6 +91,16 @@ __device__ __forceinline__ void fx_sincos(float x, float* s, float* c) { *s = __
 __device__ __forceinline__ void fx_sincos(double x, double* s, double* c) { sincos(x, s, c); }
 __device__ __forceinline__ float  fx_exp(float x)  { return __expf(x); }
 __device__ __forceinline__ double fx_exp(double x) { return exp(x); }
+// x / c for a compile-time constant c: a multiply by the rounded reciprocal in f32 (<= 1 ulp
+// apart from the IEEE quotient), the IEEE division in f64
+__device__ __forceinline__ float  fx_cdiv(float x, double c)  { return x * (float)(1.0 / c); }
+__device__ __forceinline__ double fx_cdiv(double x, double c) { return x / c; }
+// a / b via the hardware reciprocal (1 ulp) in f32; IEEE in f64
+__device__ __forceinline__ float  fx_div(float a, float b)  { return a * __builtin_amdgcn_rcpf(b); }
+__device__ __forceinline__ double fx_div(double a, double b) { return a / b; }
+// hardware square root (1 ulp) in f32; IEEE in f64
+__device__ __forceinline__ float  fx_sqrt(float x)  { return __builtin_amdgcn_sqrtf(x); }
+__device__ __forceinline__ double fx_sqrt(double x) { return sqrt(x); }
 
 template <typename T> __device__ __forceinline__ T m_clip(T x, T lo, T hi) {
   // np.clip(x, lo, hi) == minimum(maximum(x, lo), hi)
@@ -227,10 +239,13 @@ struct Philox {
 template <typename R>
 __device__ __forceinline__ void asmc_substep(R (&s)[kAsmcN], R a0, R a1, R& x, R& y, R& psi,
                                              R& u, R& v, R& r) {
-  const R speed = m_hypot(u, v);
-  const R beta = m_asin(v / (R(0.001) + speed));                          // :72
+  // f32 build: hardware sqrt / reciprocal / sin / cos and constant reciprocals (the f64 build
+  // keeps IEEE division and libm, bit-exact vs the oracle); hypot == sqrt(u^2 + v^2) here
+  const R vmag = fx_sqrt(u * u + v * v);
+  const R speed = std::is_same<R, float>::value ? vmag : m_hypot(u, v);
+  const R beta = m_asin(fx_div(v, R(0.001) + speed));                     // :72
   const R psi_d = psi + beta + a1;                                         // :73-77
-  R r_d = (psi_d - s[0]) / R(H);                                           // :84
+  R r_d = fx_cdiv(psi_d - s[0], H);                                        // :84
   s[0] = psi_d;
   const R o_dd = ((r_d - s[1]) * R(F1) - R(F3) * s[2]) * R(F2);            // :86
   const R o_d = R(H) * (o_dd + s[3]) / R(2) + s[2];                        // :87
@@ -240,11 +255,10 @@ __device__ __forceinline__ void asmc_substep(R (&s)[kAsmcN], R a0, R a1, R& x, R
   const bool fast = m_abs(u) > R(1.2);                                     // :95-99
   const R xu = fast ? R(64.55) : R(-25.0);
   const R xuu = fast ? R(-70.92) : R(0.0);
-  const R vmag = m_sqrt(u * u + v * v);
   const R yv = R(YV_K) * m_abs(v);                                         // :101-102
   const R yr = R(YR_K) * vmag, nv = R(NV_K) * vmag, nr = R(NR_K) * vmag;  // :103-108
-  const R f_u = (R(MASS - Y_V_DOT) * v * r + (xuu * m_abs(u) + xu * u)) / R(MASS - X_U_DOT);  // :113
-  const R f_psi = (R(-X_U_DOT + Y_V_DOT) * u * v + nr * r) / R(IZ - N_R_DOT);                 // :115
+  const R f_u = fx_cdiv(R(MASS - Y_V_DOT) * v * r + (xuu * m_abs(u) + xu * u), MASS - X_U_DOT);  // :113
+  const R f_psi = fx_cdiv(R(-X_U_DOT + Y_V_DOT) * u * v + nr * r, IZ - N_R_DOT);                 // :115
   const R e_psi = wrap_once(psi_d - psi);                                  // :119-120
   const R e_psi_dot = r_d - r;                                             // :121
   const R e_u = a0 - u;                                                    // :128
@@ -257,12 +271,12 @@ __device__ __forceinline__ void asmc_substep(R (&s)[kAsmcN], R a0, R a1, R& x, R
   s[14] = R(H) * (kdu + s[11]) / R(2) + s[14];                             // :143
   s[15] = R(H) * (kdp + s[12]) / R(2) + s[15];                             // :146
   s[11] = kdu; s[12] = kdp;
-  const R ua_u = -s[14] * m_sqrt(m_abs(sig_u)) * m_sign(sig_u) - R(K2_U) * sig_u;    // :150
-  const R ua_p = -s[15] * m_sqrt(m_abs(sig_p)) * m_sign(sig_p) - R(K2_PSI) * sig_p;  // :151
+  const R ua_u = -s[14] * fx_sqrt(m_abs(sig_u)) * m_sign(sig_u) - R(K2_U) * sig_u;   // :150
+  const R ua_p = -s[15] * fx_sqrt(m_abs(sig_p)) * m_sign(sig_p) - R(K2_PSI) * sig_p; // :151
   const R tx = (R(LAMBDA_U) * e_u - f_u - ua_u) * R(MASS - X_U_DOT);      // :154
   const R tz = (R(LAMBDA_PSI) * e_psi - f_psi - ua_p) * R(IZ - N_R_DOT);  // :155
-  const R tport = tx / R(2) + tz / R(B_TH);                                // :158
-  const R tstbd = tx / R(2 * C_TH) - tz / R(B_TH * C_TH);                  // :159
+  const R tport = tx / R(2) + fx_cdiv(tz, B_TH);                           // :158
+  const R tstbd = fx_cdiv(tx, 2 * C_TH) - fx_cdiv(tz, B_TH * C_TH);        // :159
   const R t0 = tport + R(C_TH) * tstbd;                                    // :176
   const R t2 = R(0.5 * B_TH) * (tport - R(C_TH) * tstbd);
   // rhs = T - C(nu) nu - D(nu) nu with C = CRB + CA (:201-211), D = Dl - Dn (:213-223)
@@ -287,7 +301,7 @@ __device__ __forceinline__ void asmc_substep(R (&s)[kAsmcN], R a0, R a1, R& x, R
   r = R(H) * (rd + s[9]) / R(2) + r;
   s[7] = ud; s[8] = vd; s[9] = rd;
   R sp, cp;
-  m_sincos(psi, &sp, &cp);                                                 // J(psi_old) :179
+  fx_sincos(psi, &sp, &cp);                                                // J(psi_old) :179
   const R xd = cp * u - sp * v, yd = sp * u + cp * v, pd = r;              // :233
   x = R(H) * (xd + s[4]) / R(2) + x;                                       // :234
   y = R(H) * (yd + s[5]) / R(2) + y;
