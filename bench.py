@@ -242,7 +242,7 @@ def main():
         if args.env_id in LEGACY_IDS:
             out["config"].pop("lidar")
             out["config"].pop("mean_obstacles")
-        if not args.no_cpu_baseline:
+        if not args.no_cpu_baseline and world == 1:        # the CPU leg runs at N = 1 only
             procs = args.cpu_procs or min(16, len(os.sched_getaffinity(0)))
             out["cpu_baseline"] = cpu_baseline(args.env_id, args.cpu_seconds, procs)
         else:
