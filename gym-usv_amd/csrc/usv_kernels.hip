@@ -54,6 +54,9 @@ template <typename R> struct State {
   const R* ray_tab;        // [128][2] (cos, sin)(start + i*res)
   R4<R>* pose;             // [N][2] pose record after the step's dynamics (split step):
                            //   (x, y, sin psi, cos psi), (partial reward, n_obs, truncated, 0)
+  uint32_t* nprng;         // [10][fstride] NumPy PCG64 per env (state hi/lo, inc hi/lo as 32-bit
+                           //   words, has_uint32, uinteger) for the NumPy-exact reset
+  int np_reset;            // 1: resets draw from NumPy's Generator(PCG64) (np_reset), not Philox
   int N, cap, limit, autoreset;
   int prio;                // scan loops: raise the issue priority of lagging waves (s_setprio)
   int fstride;             // elements between fields (>= N, 256-B aligned)
@@ -204,6 +207,7 @@ __device__ __forceinline__ void philox_uniforms(Philox& g, int l, Uni4<double>& 
 
 template <typename R, int MODE>
 __device__ __forceinline__ void reset_wave(const State<R>& S, int e, float* row) {
+  if (S.np_reset) return;                  // NumPy-exact mode: np_autoreset_kernel resets after the step
   const int l = lane_id();
   const int ep = uniform(S.I(I_EPISODE)[e]);
   Philox g(S.seed, S.gid0 + (uint64_t)e, (uint32_t)ep);
@@ -271,6 +275,147 @@ __device__ __forceinline__ void reset_wave(const State<R>& S, int e, float* row)
 // sin/cos of the heading used by the lidar; the step kernel and the reset kernel (stale scan)
 // must use this same function so their scans are bit-identical
 template <typename R> __device__ __forceinline__ void heading_sincos(R psi, R* s, R* c) { fx_sincos(psi, s, c); }
+
+// --------------------------------------------------------------------------- NumPy-exact reset
+// numpy.random.Generator(PCG64) as the reference's reset uses it (simple_env.py:234-290), one lane
+// per env, draws in the reference order: PCG64 (128-bit LCG, XSL-RR output, stepped before each
+// output), next_uint32 buffering the high half, next_double = (next64 >> 11) * 2^-53, the
+// ziggurat standard normal over NumPy's tables, uniform = lo + (hi - lo) * next_double and
+// Lemire's 32-bit bounded integers.  oracle/np_rng.py restates it and is checked against numpy.
+#include "np_ziggurat.inc"
+struct NpPcg64 {
+  uint64_t sh, sl, ih, il;
+  uint32_t has32, u32;
+  __device__ uint64_t next64() {
+    constexpr uint64_t kMh = 2549297995355413924ULL, kMl = 4865540595714422341ULL;
+    const uint64_t lo = sl * kMl;
+    const uint64_t hi = __umul64hi(sl, kMl) + sl * kMh + sh * kMl;
+    const uint64_t nlo = lo + il;
+    sh = hi + ih + (nlo < lo ? 1ULL : 0ULL);
+    sl = nlo;
+    const uint64_t x = sh ^ sl;
+    const unsigned rot = (unsigned)(sh >> 58);
+    return (x >> rot) | (x << ((64u - rot) & 63u));
+  }
+  __device__ uint32_t next32() {
+    if (has32) { has32 = 0; return u32; }
+    const uint64_t v = next64();
+    has32 = 1;
+    u32 = (uint32_t)(v >> 32);
+    return (uint32_t)v;
+  }
+  __device__ double next_double() { return (double)(next64() >> 11) * (1.0 / 9007199254740992.0); }
+  __device__ double standard_normal() {
+    constexpr double kR = 3.6541528853610088, kInvR = 0.27366123732975828;
+    for (;;) {
+      uint64_t r = next64();
+      const int idx = (int)(r & 0xff);
+      r >>= 8;
+      const bool neg = r & 1;
+      const uint64_t rabs = (r >> 1) & 0x000fffffffffffffULL;
+      double x = (double)rabs * kNpZigWi[idx];
+      if (neg) x = -x;
+      if (rabs < kNpZigKi[idx]) return x;
+      if (idx == 0) {
+        for (;;) {
+          const double xx = -kInvR * log1p(-next_double());
+          const double yy = -log1p(-next_double());
+          if (yy + yy > xx * xx) return ((rabs >> 8) & 1) ? -(kR + xx) : kR + xx;
+        }
+      }
+      if ((kNpZigFi[idx - 1] - kNpZigFi[idx]) * next_double() + kNpZigFi[idx] < exp(-0.5 * x * x)) return x;
+    }
+  }
+  __device__ double uniform(double lo, double hi) { return lo + (hi - lo) * next_double(); }
+  __device__ int integers(int lo, int hi) {                  // [lo, hi), hi - lo <= 2^32
+    const uint32_t rng = (uint32_t)(hi - 1 - lo), excl = rng + 1;
+    uint64_t m = (uint64_t)next32() * excl;
+    uint32_t left = (uint32_t)m;
+    if (left < excl) {
+      const uint32_t thr = (0xFFFFFFFFu - rng) % excl;
+      while (left < thr) { m = (uint64_t)next32() * excl; left = (uint32_t)m; }
+    }
+    return lo + (int)(m >> 32);
+  }
+};
+
+template <typename R>
+__device__ __forceinline__ NpPcg64 np_load(const State<R>& S, int e) {
+  auto w = [&](int i) { return (uint64_t)S.nprng[(size_t)i * S.fstride + e]; };
+  return NpPcg64{w(0) | (w(1) << 32), w(2) | (w(3) << 32), w(4) | (w(5) << 32), w(6) | (w(7) << 32),
+                 (uint32_t)w(8), (uint32_t)w(9)};
+}
+template <typename R>
+__device__ __forceinline__ void np_store(const State<R>& S, int e, const NpPcg64& g) {
+  const uint32_t v[10] = {(uint32_t)g.sh, (uint32_t)(g.sh >> 32), (uint32_t)g.sl, (uint32_t)(g.sl >> 32),
+                          (uint32_t)g.ih, (uint32_t)(g.ih >> 32), (uint32_t)g.il, (uint32_t)(g.il >> 32),
+                          g.has32, g.u32};
+  for (int i = 0; i < 10; ++i) S.nprng[(size_t)i * S.fstride + e] = v[i];
+}
+
+// UsvSimpleEnv.reset (simple_env.py:228-308) with the env's own Generator; usv-asmc-simple also
+// zeroes the ASMC state (simple_env_asmc.py:14-16).  Writes the reset obs header into `row`
+// (its sensor half, the stale scan, is the caller's).  Draws in double, stored as R.
+template <typename R, int MODE>
+__device__ void np_reset(const State<R>& S, int e, float* row) {
+  NpPcg64 g = np_load(S, e);
+  const double sx = 0.5 * g.standard_normal() + kBound / 2;                      // :234-235
+  const double sy = 0.5 * g.standard_normal() + kBound / 2;
+  (void)g.standard_normal(); (void)g.standard_normal(); (void)g.next_double();   // :236-237, discarded
+  const double psi = g.uniform(-kPi, kPi);                                       // :238
+  const double ang = g.uniform(-kPi, kPi), dist = g.uniform(100, 110);           // :241-242
+  const double tx = g.uniform(0, kBound), ty = g.uniform(0, kBound);             // :245
+  const double u = g.uniform(0.0, 0.15), v = g.uniform(0.0, 0.15), r = g.uniform(0.0, 0.15);  // :246
+  const double mu = g.uniform(1.50, 3);                                          // :249
+  (void)g.next_double(); (void)g.next_double();                                  // max_action[1], [2]
+  const double mr = g.uniform(3, 6);                                             // :250
+  const double refv = g.uniform(0.75, mu);                                       // :251
+  const int n = g.integers(15, 30);                                              // :257
+  R4<R>* ob = S.obst + (size_t)e * S.cap;
+  int cnt = 0;
+  for (int j = 0; j < n; ++j) {                                                  // :258-268
+    const double ox = g.uniform(0, kBound), oy = g.uniform(0, kBound);
+    if (!(hypot(sx - ox, sy - oy) < 0.5 || hypot(tx - ox, ty - oy) < 0.5)) ob[cnt++] = R4<R>{R(ox), R(oy), R(0), R(0)};
+  }
+  if (cnt == 0) {                                                                // :270-274
+    const double ox = g.uniform(0, kBound), oy = g.uniform(0, kBound);
+    ob[cnt++] = R4<R>{R(ox), R(oy), R(0), R(0)};
+  }
+  for (int j = 0; j < cnt; ++j) {                                                // :290
+    const R rad = R(g.uniform(0.15, 0.5));
+    ob[j].z = rad;
+    ob[j].w = rad * rad;
+  }
+  for (int j = cnt; j < S.cap; ++j) ob[j] = R4<R>{R(0), R(0), R(0), R(0)};
+  np_store(S, e, g);
+  if (MODE == USV_MODE_ASMC_SIMPLE)
+    for (int i = 0; i < kAsmcN; ++i) S.asmc[(size_t)i * S.N + e] = R(0);
+  const R x0 = R(sx), y0 = R(sy), ps = R(psi);
+  S.F(F_X)[e] = x0; S.F(F_Y)[e] = y0; S.F(F_PSI)[e] = ps;
+  S.F(F_U)[e] = R(u); S.F(F_V)[e] = R(v); S.F(F_R)[e] = R(r);
+  S.F(F_PROGRESS)[e] = R(0);
+  S.F(F_PX0)[e] = x0; S.F(F_PY0)[e] = y0;
+  S.F(F_PX1)[e] = R(sx + cos(ang) * dist); S.F(F_PY1)[e] = R(sy + sin(ang) * dist);   // :243
+  S.F(F_MAX_U)[e] = R(mu); S.F(F_MAX_R)[e] = R(mr); S.F(F_REF_V)[e] = R(refv);
+  S.I(I_NOBS)[e] = cnt;
+  S.I(I_ELAPSED)[e] = 0;
+  S.I(I_EPISODE)[e] = S.I(I_EPISODE)[e] + 1;
+  S.I(I_SCAN)[e] = 0;
+  const R angle = wrap_angle(m_atan2(R(ty) - y0, R(tx) - x0) - ps);             // :302, :63-80
+  const R dst = m_hypot(x0 - R(tx), y0 - R(ty));
+  float h[kHdr];
+  make_header<R>(h, R(u), R(v), R(r), angle, dst, R(0), R(refv), R(0), R(0), R(mu), R(mr));
+  for (int i = 0; i < kHdr; ++i) row[i] = h[i];
+}
+
+// Same-step autoreset in NumPy-exact mode, after the step kernel: envs that ended this step get
+// a reset header; their obs row keeps the step's scan as the stale sensors (simple_env.py:302).
+template <typename R, int MODE>
+__global__ __launch_bounds__(kBlock) void np_autoreset_kernel(State<R> S, IO<R> io) {
+  const int e = blockIdx.x * kBlock + threadIdx.x;
+  if (e >= S.N || !(io.term[e] | io.trunc[e])) return;
+  np_reset<R, MODE>(S, e, io.obs + (size_t)e * kObsDim);
+}
 
 // --------------------------------------------------------------------------- phase 1
 // UsvSimpleEnv.step kinematics..reward terms (simple_env.py:310-346); for usv-asmc-simple
@@ -1425,7 +1570,11 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(State<R> S, IO<R> io) {
     float* row = io.obs + (size_t)e * kObsDim;
     row[kHdr + l] = (float)l_norm(rd0);
     row[kHdr + 64 + l] = (float)l_norm(rd1);
-    reset_wave<R, MODE>(S, e, row);
+    if (S.np_reset) {
+      if (l == 0) np_reset<R, MODE>(S, e, row);
+    } else {
+      reset_wave<R, MODE>(S, e, row);
+    }
   }
 }
 
@@ -1764,7 +1913,7 @@ const FieldDesc kFields[USV_FIELD_COUNT] = {
     {"progress", 0}, {"path_x0", 0}, {"path_y0", 0}, {"path_x1", 0}, {"path_y1", 0},
     {"max_u", 0}, {"max_r", 0}, {"ref_v", 0}, {"n_obs", 1}, {"elapsed", 1}, {"episode", 1},
     {"scan_valid", 1}, {"obs_x", 0}, {"obs_y", 0}, {"obs_r", 0}, {"sensor_last", 0}, {"asmc", 0},
-    {"v0_last", 0}, {"v0_aux", 0}, {"v0_target", 0}, {"v0_action_last", 0}, {"v0_ye", 0}};
+    {"v0_last", 0}, {"v0_aux", 0}, {"v0_target", 0}, {"v0_action_last", 0}, {"v0_ye", 0}, {"np_rng", 1}};
 
 bool is_legacy(int mode) {   // lane-per-env legacy envs: obs 6, scalar action, no lidar
   return mode == USV_MODE_ASMC_V0 || mode == USV_MODE_ASMC_YE_INT_V0 || mode == USV_MODE_PID_V0;
@@ -1804,7 +1953,7 @@ int carve(Handle* h, State<R>& S) {
   const size_t bytes = F_NREAL * stride * sizeof(R) + al(I_NINT * stride * 4) +
                        al(N * cap * sizeof(R4<R>)) + al(N * kSensors * sizeof(R)) +
                        al((size_t)kAsmcN * N * sizeof(R)) + al((size_t)kV0N * stride * sizeof(R)) +
-                       al(2 * kSensors * sizeof(R)) + al(2 * N * sizeof(R4<R>));
+                       al(2 * kSensors * sizeof(R)) + al(2 * N * sizeof(R4<R>)) + al(10 * stride * 4);
   HIP_TRY(hipMalloc(&h->slab, bytes));
   HIP_TRY(hipMemset(h->slab, 0, bytes));
   char* p = (char*)h->slab;
@@ -1819,6 +1968,8 @@ int carve(Handle* h, State<R>& S) {
   R* tab = (R*)take(2 * kSensors * sizeof(R));
   S.ray_tab = tab;
   S.pose = (R4<R>*)take(2 * N * sizeof(R4<R>));
+  S.nprng = (uint32_t*)take(10 * stride * 4);
+  S.np_reset = 0;
   S.N = h->cfg.num_envs;
   S.cap = h->cfg.obstacle_cap;
   S.limit = h->cfg.max_episode_steps;
@@ -1925,8 +2076,28 @@ void* pick_q(int mode, bool fused, int qe) {
 }
 
 template <typename R>
+int launch_step_kernels(Handle* h, State<R>& S, const float* act, float* obs, void* rew, uint8_t* term,
+                        uint8_t* trunc, float* fobs, hipStream_t st);
+
+// The step, then (NumPy-exact reset mode) the resets of the envs that ended in it.
+template <typename R>
 int launch_step(Handle* h, State<R>& S, const float* act, float* obs, void* rew, uint8_t* term,
                 uint8_t* trunc, float* fobs, hipStream_t st) {
+  const int rc = launch_step_kernels(h, S, act, obs, rew, term, trunc, fobs, st);
+  if (rc != USV_OK || !S.np_reset || S.autoreset != USV_AUTORESET_SAME_STEP) return rc;
+  IO<R> io{act, obs, (R*)rew, term, trunc, fobs, nullptr};
+  const dim3 grid((S.N + kBlock - 1) / kBlock), block(kBlock);
+  if (h->cfg.mode == USV_MODE_SIMPLE)
+    hipLaunchKernelGGL((np_autoreset_kernel<R, USV_MODE_SIMPLE>), grid, block, 0, st, S, io);
+  else
+    hipLaunchKernelGGL((np_autoreset_kernel<R, USV_MODE_ASMC_SIMPLE>), grid, block, 0, st, S, io);
+  HIP_TRY(hipGetLastError());
+  return USV_OK;
+}
+
+template <typename R>
+int launch_step_kernels(Handle* h, State<R>& S, const float* act, float* obs, void* rew, uint8_t* term,
+                        uint8_t* trunc, float* fobs, hipStream_t st) {
   IO<R> io{act, obs, (R*)rew, term, trunc, fobs, nullptr};
   if (is_legacy(h->cfg.mode)) {
     const dim3 grid((S.N + kBlock - 1) / kBlock), block(kBlock);
@@ -2014,6 +2185,7 @@ int field_per_env(const Handle* h, int f) {
   if (f == USV_FIELD_V0_AUX) return 3;
   if (f == USV_FIELD_V0_TARGET) return 6;
   if (f == USV_FIELD_V0_YE) return 2;
+  if (f == USV_FIELD_NP_RNG) return 10;
   return 1;
 }
 
@@ -2092,6 +2264,21 @@ int field_io(Handle* h, State<R>& S, int f, void* host, bool to_host) {
       for (size_t e = 0; e < N; ++e)
         for (int i = 0; i < kAsmcN; ++i) tmp[(size_t)i * N + e] = (R)hd[e * kAsmcN + i];
       HIP_TRY(hipMemcpy(S.asmc, tmp.data(), cnt * sizeof(R), hipMemcpyHostToDevice));
+    }
+    return USV_OK;
+  }
+  if (f == USV_FIELD_NP_RNG) {   // device SoA uint32 rows, host [N][10] int32
+    std::vector<uint32_t> tmp(N);
+    uint32_t* hd = (uint32_t*)host;
+    for (int i = 0; i < 10; ++i) {
+      uint32_t* d = S.nprng + (size_t)i * S.fstride;
+      if (to_host) {
+        HIP_TRY(hipMemcpy(tmp.data(), d, N * 4, hipMemcpyDeviceToHost));
+        for (size_t e = 0; e < N; ++e) hd[e * 10 + i] = tmp[e];
+      } else {
+        for (size_t e = 0; e < N; ++e) tmp[e] = hd[e * 10 + i];
+        HIP_TRY(hipMemcpy(d, tmp.data(), N * 4, hipMemcpyHostToDevice));
+      }
     }
     return USV_OK;
   }
@@ -2241,6 +2428,16 @@ int usv_act_dim(void* hp) {
 }
 int usv_reward_bytes(void* hp) {
   return hp ? (as_handle(hp)->cfg.precision == USV_F64 ? 8 : 4) : fail(USV_ERR_ARG, "null handle");
+}
+
+int usv_set_reset_rng(void* hp, int32_t kind) {
+  Handle* h = as_handle(hp);
+  if (!h) return fail(USV_ERR_ARG, "null handle");
+  if (kind != USV_RESET_PHILOX && kind != USV_RESET_NUMPY_PCG64) return fail(USV_ERR_ARG, "unknown reset rng");
+  if (kind == USV_RESET_NUMPY_PCG64 && h->cfg.mode != USV_MODE_SIMPLE && h->cfg.mode != USV_MODE_ASMC_SIMPLE)
+    return fail(USV_ERR_ARG, "the NumPy-exact reset exists for usv-simple and usv-asmc-simple only");
+  h->sf.np_reset = h->sd.np_reset = kind == USV_RESET_NUMPY_PCG64;
+  return USV_OK;
 }
 
 int usv_seed(void* hp, uint64_t seed) {

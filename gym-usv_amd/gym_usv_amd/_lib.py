@@ -19,6 +19,7 @@ MODE_SIMPLE, MODE_ASMC_SIMPLE, MODE_ASMC_V0, MODE_ASMC_YE_INT_V0, MODE_PID_V0 = 
 F32, F64 = 0, 1
 AUTORESET_SAME_STEP, AUTORESET_DISABLED = 0, 1
 LIDAR_BRUTE, LIDAR_WINDOW = 0, 1
+RESET_PHILOX, RESET_NUMPY_PCG64 = 0, 1
 OBS_DIM, SENSOR_COUNT, ACT_DIM, ASMC_STATE = 143, 128, 2, 16
 
 
@@ -47,6 +48,7 @@ SIGNATURES = [
     ("usv_act_dim", ctypes.c_int, [_vp]),
     ("usv_reward_bytes", ctypes.c_int, [_vp]),
     ("usv_seed", ctypes.c_int, [_vp, _u64]),
+    ("usv_set_reset_rng", ctypes.c_int, [_vp, _i32]),
     ("usv_reset", ctypes.c_int, [_vp, _vp, _vp, _vp]),
     ("usv_step", ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     ("usv_field_info", ctypes.c_int, [_vp, _i32, ctypes.POINTER(_i32), ctypes.POINTER(_i32),

@@ -39,6 +39,20 @@ def _spaces(env_id):
             Box(np.array([0.2, -1]), np.array([1, 1]), shape=(2,), dtype=np.float32))
 
 
+def np_rng_words(seeds):
+    """USV_FIELD_NP_RNG rows for numpy Generator(PCG64(SeedSequence(seed))) per seed: the state
+    and increment as 32-bit halves, has_uint32, uinteger (include/usv_hip.h)."""
+    out = np.zeros((len(seeds), 10), dtype=np.uint32)
+    m64, m32 = (1 << 64) - 1, (1 << 32) - 1
+    for i, sd in enumerate(seeds):
+        st = np.random.PCG64(np.random.SeedSequence(int(sd))).state
+        a, b = st["state"]["state"], st["state"]["inc"]
+        for k, w in enumerate((a >> 64, a & m64, b >> 64, b & m64)):
+            out[i, 2 * k], out[i, 2 * k + 1] = w & m32, w >> 32
+        out[i, 8], out[i, 9] = st["has_uint32"], st["uinteger"]
+    return out.view(np.int32)
+
+
 def _stream_ptr(device):
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
@@ -62,7 +76,7 @@ class UsvVectorEnv:
 
     def __init__(self, env_id="usv-simple", num_envs=4096, device=0, seed=0, precision="f32",
                  autoreset=True, max_episode_steps=None, obstacle_cap=32, lidar="window",
-                 env_id_offset=0):
+                 env_id_offset=0, reset_rng="philox"):
         if env_id not in ENV_SPECS:
             raise ValueError(f"unknown env id {env_id!r}; known: {sorted(ENV_SPECS)}")
         if not torch.cuda.is_available():
@@ -98,12 +112,31 @@ class UsvVectorEnv:
         self.max_episode_steps = cfg.max_episode_steps
         self.single_observation_space, self.single_action_space = _spaces(env_id)
         self._fields = self._field_table()
+        if reset_rng not in ("philox", "numpy"):
+            raise ValueError("reset_rng must be 'philox' or 'numpy'")
+        self.reset_rng = reset_rng
+        self._np_seeded = False
+        if reset_rng == "numpy":
+            _lib.check(self.lib.usv_set_reset_rng(self._h, _lib.RESET_NUMPY_PCG64))
 
     # ------------------------------------------------------------------ API
     def reset(self, seed=None, options=None, mask=None):
         if options:
             raise NotImplementedError("reset options (place_obstacles_on_path) are not supported yet")
-        if seed is not None:
+        if self.reset_rng == "numpy":
+            # each env owns a numpy Generator(PCG64(SeedSequence(seed_i))), like gymnasium's
+            # Env.reset(seed) (simple_env.py:229); an int seed gives env i seed + global id (the
+            # make_vec_env / DummyVecEnv convention), a sequence gives one seed per env
+            if seed is None and not self._np_seeded:
+                seed = int(self.cfg.seed)
+            if seed is not None:
+                if np.ndim(seed) == 0:
+                    seeds = int(seed) + int(self.cfg.env_id_offset) + np.arange(self.num_envs)
+                else:
+                    seeds = np.asarray(seed, dtype=np.int64).reshape(self.num_envs)
+                self.set_field("np_rng", np_rng_words(seeds))
+                self._np_seeded = True
+        elif seed is not None:
             _lib.check(self.lib.usv_seed(self._h, ctypes.c_uint64(int(seed))))
         m = None
         if mask is not None:

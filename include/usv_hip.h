@@ -75,6 +75,13 @@ typedef enum usv_autoreset {
   USV_AUTORESET_DISABLED = 1   /* done envs keep stepping until usv_reset(mask)       */
 } usv_autoreset;
 
+typedef enum usv_reset_rng {
+  USV_RESET_PHILOX = 0,      /* Philox4x32-10 keyed by (seed, global env id, episode): the
+                                reference's reset distributions, not its streams (default)   */
+  USV_RESET_NUMPY_PCG64 = 1  /* each env's own numpy Generator(PCG64) (USV_FIELD_NP_RNG), drawn
+                                in the reference's order: resets equal the reference's        */
+} usv_reset_rng;
+
 typedef enum usv_lidar_algo {
   USV_LIDAR_BRUTE = 0,  /* every (ray, obstacle) pair                         */
   USV_LIDAR_WINDOW = 1  /* angular-window pruning, bit-identical to BRUTE    */
@@ -116,6 +123,10 @@ typedef enum usv_field {
   USV_FIELD_V0_TARGET,      /* [6]  usv-asmc-v0 `target` (x_0, y_0, speed, ak, x_d, y_d)  */
   USV_FIELD_V0_ACTION_LAST, /* [1]  usv-asmc-v0 state[5] (previous action)                 */
   USV_FIELD_V0_YE,          /* [2]  usv-asmc-ye-int-v0 aux_vars[3] ye_int, last[9] ye_last  */
+  USV_FIELD_NP_RNG,         /* int [10]: the env's numpy Generator(PCG64) for USV_RESET_NUMPY_PCG64:
+                               state high / low and increment high / low 64-bit words as
+                               little-endian 32-bit halves, has_uint32, uinteger
+                               (bit_generator.state of np.random.PCG64)                    */
   USV_FIELD_COUNT
 } usv_field;
 
@@ -138,6 +149,11 @@ int usv_reward_bytes(void* handle);
 /* Re-key the reset RNG (Philox4x32-10, key = seed, counter = global env id / episode)
  * and zero every episode counter.  Host-side only; no launch. */
 int usv_seed(void* handle, uint64_t seed);
+
+/* Select the reset RNG (usv_reset_rng) <- Env.reset(seed) seeding np_random
+ * (simple_env.py:229, gymnasium seeding.np_random); NUMPY_PCG64 for usv-simple and
+ * usv-asmc-simple only.  The generator states are set through USV_FIELD_NP_RNG. */
+int usv_set_reset_rng(void* handle, int32_t kind);
 
 /* Reset envs whose mask byte is non-zero (all envs if mask_dev == NULL) and write their
  * reset observation rows into obs_dev [num_envs][obs_dim] (other rows untouched). */

@@ -616,3 +616,54 @@ def test_legacy_f64_reset_distribution(env_id, family, fname):
         assert p > 1e-4, name
     assert np.all(g["v0_ye"] == 0) and np.all(obs[:, [0, 1, 2, 5]] == 0)
     env.close()
+
+
+# --------------------------------------------------------------------------- NumPy-exact reset
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+@pytest.mark.parametrize("fname,env_id", [("simple_traj.npz", "usv-simple"), ("simple_traj_tl.npz", "usv-simple"),
+                                          ("asmc_simple_traj.npz", "usv-asmc-simple")])
+def test_np_reset_full_trajectory(golden, fname, env_id, precision):
+    """reset_rng="numpy": every env draws its resets from its own Generator(PCG64(SeedSequence(
+    seed))) in the reference's order (simple_env.py:228-308), so the reference's rollouts replay
+    whole, across TimeLimit truncations and terminations with same-step autoreset.
+    f64: the seeded reset state equals the reference's exactly and the full rollout matches at the
+    golden tolerances; f32: the reset state is the reference's rounded to float32."""
+    g = golden(fname)
+    n, T = g["actions"].shape[:2]
+    limit = int(g["limit"])
+    env = make(env_id, n, precision=precision, max_episode_steps=max(limit, 0), reset_rng="numpy")
+    obs, _ = env.reset(seed=g["seeds"])
+    (obs,) = to_np(obs)
+    st = env.get_state()
+    ref = golden_state(g)
+    keys = ("x", "y", "psi", "u", "v", "r", "path_x0", "path_y0", "path_x1", "path_y1", "max_u",
+            "max_r", "ref_v", "obs_x", "obs_y", "obs_r")
+    np.testing.assert_array_equal(st["n_obs"], ref["n_obs"])
+    for k in keys:
+        want = np.asarray(ref[k], dtype=np.float64)
+        if precision == "f32":
+            want = want.astype(np.float32).astype(np.float64)
+        np.testing.assert_array_equal(st[k], want, err_msg=k)
+    if precision == "f64":
+        np.testing.assert_array_equal(obs, g["obs0"])
+    else:
+        np.testing.assert_allclose(obs, g["obs0"], atol=2e-6, rtol=0)
+        env.close()
+        return
+    worst = {"obs": 0.0, "fobs": 0.0, "rew": 0.0}
+    resets = 0
+    for t in range(T):
+        o, r, te, tr, info = env.step(torch.from_numpy(g["actions"][:, t]).cuda())
+        o, r, te, tr, fo = to_np(o, r, te, tr, info["final_obs"])
+        np.testing.assert_array_equal(te, g["terminated"][:, t], err_msg=f"t={t}")
+        np.testing.assert_array_equal(tr, g["truncated"][:, t], err_msg=f"t={t}")
+        done = te | tr
+        resets += int(done.sum())
+        worst["obs"] = max(worst["obs"], float(np.abs(o - g["obs"][:, t]).max()))
+        worst["rew"] = max(worst["rew"], float(np.abs(r - g["reward"][:, t]).max()))
+        if done.any():
+            worst["fobs"] = max(worst["fobs"], float(np.abs(fo[done] - g["final_obs"][done, t]).max()))
+    print(f"\n[np-reset {fname} {env_id}] {resets} in-kernel resets over {n}x{T} steps; max err {worst}")
+    assert resets > 0
+    assert worst["obs"] <= 2e-6 and worst["fobs"] <= 2e-6 and worst["rew"] <= 1e-8, worst
+    env.close()
