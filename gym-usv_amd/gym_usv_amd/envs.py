@@ -4,7 +4,10 @@
 (gym_usv/envs/simple_env.py:7, simple_env_asmc.py:7): ``reset(seed=None, options=None) ->
 (obs float32[143], info)`` and ``step(action) -> (obs, reward, terminated, truncated, info)``
 with NumPy in/out.  Each is a 1-env ``UsvVectorEnv`` with autoreset off and no TimeLimit
-(``gym_usv_amd.make`` adds the registered TimeLimit, like ``gymnasium.make``).  They exist for
+(``gym_usv_amd.make`` adds the registered TimeLimit, like ``gymnasium.make``).  With
+``reset_rng="numpy"`` a usv-simple / usv-asmc-simple env draws its resets from
+``Generator(PCG64(SeedSequence(seed)))`` exactly like the reference, so ``reset(seed=s)`` followed by
+the same actions reproduces the reference's episode.  They exist for
 API compatibility and debugging; throughput lives in ``UsvVectorEnv``.
 """
 from __future__ import annotations
@@ -20,14 +23,14 @@ class _SingleEnv:
     metadata = {"render_modes": [], "render_fps": 30}
 
     def __init__(self, render_mode=None, options=None, device=0, precision="f32",
-                 max_episode_steps=0, seed=None):
+                 max_episode_steps=0, seed=None, reset_rng="philox"):
         if render_mode not in (None,):
             raise NotImplementedError("rendering is out of scope (SURVEY.md §2 #13)")
         self.render_mode = render_mode
         self.options = options or {}
         self._venv = UsvVectorEnv(self.env_id, num_envs=1, device=device, precision=precision,
                                   autoreset=False, max_episode_steps=max_episode_steps,
-                                  seed=0 if seed is None else seed)
+                                  seed=0 if seed is None else seed, reset_rng=reset_rng)
         self.observation_space = self._venv.single_observation_space
         self.action_space = self._venv.single_action_space
         self._seeded = False

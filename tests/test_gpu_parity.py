@@ -667,3 +667,20 @@ def test_np_reset_full_trajectory(golden, fname, env_id, precision):
     assert resets > 0
     assert worst["obs"] <= 2e-6 and worst["fobs"] <= 2e-6 and worst["rew"] <= 1e-8, worst
     env.close()
+
+
+def test_np_reset_single_env_api(golden):
+    """gym_usv_amd.make(id, reset_rng="numpy") is the reference's env: reset(seed) and the same
+    actions give its observations (usv-simple, TimeLimit 500, float64)."""
+    import gym_usv_amd
+    g = golden("simple_traj.npz")
+    env = gym_usv_amd.make("usv-simple", precision="f64", reset_rng="numpy")
+    obs, _ = env.reset(seed=int(g["seeds"][2]))
+    np.testing.assert_array_equal(obs, g["obs0"][2])
+    for t in range(40):
+        obs, r, te, tr, _ = env.step(g["actions"][2, t])
+        np.testing.assert_array_equal(obs, g["final_obs"][2, t])
+        assert abs(r - g["reward"][2, t]) <= 1e-8 and te == g["terminated"][2, t]
+        if te or tr:
+            break
+    env.close()
