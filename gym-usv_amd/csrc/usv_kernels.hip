@@ -56,7 +56,9 @@ template <typename R> struct State {
                            //   (x, y, sin psi, cos psi), (partial reward, n_obs, truncated, 0)
   uint32_t* nprng;         // [10][fstride] NumPy PCG64 per env (state hi/lo, inc hi/lo as 32-bit
                            //   words, has_uint32, uinteger) for the NumPy-exact reset
-  int np_reset;            // 1: resets draw from NumPy's Generator(PCG64) (np_reset), not Philox
+  uint32_t* npmt;          // [625][fstride] legacy envs: np.random.RandomState MT19937 key[624], pos
+  int np_reset;            // 1: resets draw from NumPy's Generator(PCG64) (np_reset) -- legacy
+                           //   envs: from np.random's MT19937 (NpMt) -- not Philox
   int N, cap, limit, autoreset;
   int prio;                // scan loops: raise the issue priority of lagging waves (s_setprio)
   int fstride;             // elements between fields (>= N, 256-B aligned)
@@ -1602,10 +1604,60 @@ __device__ __forceinline__ void v0_obs(float* row, R u, R v_ak, R r, R ye, R psi
 // FAM 1 / 2 are the float64 legacy envs on the same template: UsvAsmcYeIntEnv.reset
 // (usv_asmc_ye_int_env.py:256-296: x, y ~ U(-5, 5), speed ~ U(0.4, 1.4)) and UsvPidEnv.reset
 // (usv_pid_env.py:236-276: speed ~ U(0.4, 1.4)); the draw order is the same in all three.
+// NumPy-exact mode: np.random.uniform on the legacy global RandomState (MT19937, seeded by
+// np.random.seed), one lane per env, key[624] + pos kept in S.npmt.  uniform = lo + (hi - lo) *
+// ((a >> 5) * 2^26 + (b >> 6)) / 2^53 over two 32-bit draws (numpy's mt19937 next_double).
+struct NpMt {
+  uint32_t* k;     // key word i of this env at k[i * stride]
+  size_t stride;
+  __device__ uint32_t& key(int i) const { return k[(size_t)i * stride]; }
+  __device__ void twist() const {
+    constexpr uint32_t kA = 0x9908b0dfu, kU = 0x80000000u, kL = 0x7fffffffu;
+    int i = 0;
+    for (; i < 624 - 397; ++i) {
+      const uint32_t y = (key(i) & kU) | (key(i + 1) & kL);
+      key(i) = key(i + 397) ^ (y >> 1) ^ ((0u - (y & 1u)) & kA);
+    }
+    for (; i < 623; ++i) {
+      const uint32_t y = (key(i) & kU) | (key(i + 1) & kL);
+      key(i) = key(i + 397 - 624) ^ (y >> 1) ^ ((0u - (y & 1u)) & kA);
+    }
+    const uint32_t y = (key(623) & kU) | (key(0) & kL);
+    key(623) = key(396) ^ (y >> 1) ^ ((0u - (y & 1u)) & kA);
+    key(624) = 0;
+  }
+  __device__ uint32_t next32() const {
+    if (key(624) >= 624) twist();
+    const uint32_t p = key(624);
+    key(624) = p + 1;
+    uint32_t y = key((int)p);
+    y ^= y >> 11;
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= y >> 18;
+    return y;
+  }
+  __device__ double uniform(double lo, double hi) const {
+    const uint32_t a = next32() >> 5, b = next32() >> 6;
+    return lo + (hi - lo) * ((a * 67108864.0 + b) / 9007199254740992.0);
+  }
+};
+
+template <typename R, int FAM, typename G>
+__device__ void v0_reset_draws(const State<R>& S, int e, float* row, int ep, G&& g);
+
 template <typename R, int FAM = kFamV0>
 __device__ void v0_reset(const State<R>& S, int e, float* row) {
   const int ep = S.I(I_EPISODE)[e];
-  Philox g(S.seed, S.gid0 + (uint64_t)e, (uint32_t)ep);
+  if (S.np_reset) {
+    v0_reset_draws<R, FAM>(S, e, row, ep, NpMt{S.npmt + e, (size_t)S.fstride});
+  } else {
+    v0_reset_draws<R, FAM>(S, e, row, ep, Philox(S.seed, S.gid0 + (uint64_t)e, (uint32_t)ep));
+  }
+}
+
+template <typename R, int FAM, typename G>
+__device__ void v0_reset_draws(const State<R>& S, int e, float* row, int ep, G&& g) {
   const double lim = FAM == kFamYeInt ? 5.0 : 2.5;
   const double x = g.uniform(-lim, lim), y = g.uniform(-lim, lim);               // :260-261
   const double psi = g.uniform(-kPi, kPi);                                        // :262
@@ -1913,7 +1965,7 @@ const FieldDesc kFields[USV_FIELD_COUNT] = {
     {"progress", 0}, {"path_x0", 0}, {"path_y0", 0}, {"path_x1", 0}, {"path_y1", 0},
     {"max_u", 0}, {"max_r", 0}, {"ref_v", 0}, {"n_obs", 1}, {"elapsed", 1}, {"episode", 1},
     {"scan_valid", 1}, {"obs_x", 0}, {"obs_y", 0}, {"obs_r", 0}, {"sensor_last", 0}, {"asmc", 0},
-    {"v0_last", 0}, {"v0_aux", 0}, {"v0_target", 0}, {"v0_action_last", 0}, {"v0_ye", 0}, {"np_rng", 1}};
+    {"v0_last", 0}, {"v0_aux", 0}, {"v0_target", 0}, {"v0_action_last", 0}, {"v0_ye", 0}, {"np_rng", 1}, {"np_mt", 1}};
 
 bool is_legacy(int mode) {   // lane-per-env legacy envs: obs 6, scalar action, no lidar
   return mode == USV_MODE_ASMC_V0 || mode == USV_MODE_ASMC_YE_INT_V0 || mode == USV_MODE_PID_V0;
@@ -1953,7 +2005,8 @@ int carve(Handle* h, State<R>& S) {
   const size_t bytes = F_NREAL * stride * sizeof(R) + al(I_NINT * stride * 4) +
                        al(N * cap * sizeof(R4<R>)) + al(N * kSensors * sizeof(R)) +
                        al((size_t)kAsmcN * N * sizeof(R)) + al((size_t)kV0N * stride * sizeof(R)) +
-                       al(2 * kSensors * sizeof(R)) + al(2 * N * sizeof(R4<R>)) + al(10 * stride * 4);
+                       al(2 * kSensors * sizeof(R)) + al(2 * N * sizeof(R4<R>)) + al(10 * stride * 4) +
+                       (is_legacy(h->cfg.mode) ? al(625 * stride * 4) : 0);
   HIP_TRY(hipMalloc(&h->slab, bytes));
   HIP_TRY(hipMemset(h->slab, 0, bytes));
   char* p = (char*)h->slab;
@@ -1969,6 +2022,7 @@ int carve(Handle* h, State<R>& S) {
   S.ray_tab = tab;
   S.pose = (R4<R>*)take(2 * N * sizeof(R4<R>));
   S.nprng = (uint32_t*)take(10 * stride * 4);
+  S.npmt = is_legacy(h->cfg.mode) ? (uint32_t*)take(625 * stride * 4) : nullptr;   // legacy ids only
   S.np_reset = 0;
   S.N = h->cfg.num_envs;
   S.cap = h->cfg.obstacle_cap;
@@ -2084,7 +2138,8 @@ template <typename R>
 int launch_step(Handle* h, State<R>& S, const float* act, float* obs, void* rew, uint8_t* term,
                 uint8_t* trunc, float* fobs, hipStream_t st) {
   const int rc = launch_step_kernels(h, S, act, obs, rew, term, trunc, fobs, st);
-  if (rc != USV_OK || !S.np_reset || S.autoreset != USV_AUTORESET_SAME_STEP) return rc;
+  // (the legacy kernels reset inline, from the MT19937 state, in the NumPy-exact mode too)
+  if (rc != USV_OK || !S.np_reset || S.autoreset != USV_AUTORESET_SAME_STEP || is_legacy(h->cfg.mode)) return rc;
   IO<R> io{act, obs, (R*)rew, term, trunc, fobs, nullptr};
   const dim3 grid((S.N + kBlock - 1) / kBlock), block(kBlock);
   if (h->cfg.mode == USV_MODE_SIMPLE)
@@ -2186,6 +2241,7 @@ int field_per_env(const Handle* h, int f) {
   if (f == USV_FIELD_V0_TARGET) return 6;
   if (f == USV_FIELD_V0_YE) return 2;
   if (f == USV_FIELD_NP_RNG) return 10;
+  if (f == USV_FIELD_NP_MT) return is_legacy(h->cfg.mode) ? 625 : 0;
   return 1;
 }
 
@@ -2267,16 +2323,17 @@ int field_io(Handle* h, State<R>& S, int f, void* host, bool to_host) {
     }
     return USV_OK;
   }
-  if (f == USV_FIELD_NP_RNG) {   // device SoA uint32 rows, host [N][10] int32
+  if (f == USV_FIELD_NP_RNG || f == USV_FIELD_NP_MT) {   // device SoA uint32 rows, host [N][per] int32
+    const int per = field_per_env(h, f);
     std::vector<uint32_t> tmp(N);
     uint32_t* hd = (uint32_t*)host;
-    for (int i = 0; i < 10; ++i) {
-      uint32_t* d = S.nprng + (size_t)i * S.fstride;
+    for (int i = 0; i < per; ++i) {
+      uint32_t* d = (f == USV_FIELD_NP_RNG ? S.nprng : S.npmt) + (size_t)i * S.fstride;
       if (to_host) {
         HIP_TRY(hipMemcpy(tmp.data(), d, N * 4, hipMemcpyDeviceToHost));
-        for (size_t e = 0; e < N; ++e) hd[e * 10 + i] = tmp[e];
+        for (size_t e = 0; e < N; ++e) hd[e * per + i] = tmp[e];
       } else {
-        for (size_t e = 0; e < N; ++e) tmp[e] = hd[e * 10 + i];
+        for (size_t e = 0; e < N; ++e) tmp[e] = hd[e * per + i];
         HIP_TRY(hipMemcpy(d, tmp.data(), N * 4, hipMemcpyHostToDevice));
       }
     }
@@ -2434,8 +2491,6 @@ int usv_set_reset_rng(void* hp, int32_t kind) {
   Handle* h = as_handle(hp);
   if (!h) return fail(USV_ERR_ARG, "null handle");
   if (kind != USV_RESET_PHILOX && kind != USV_RESET_NUMPY_PCG64) return fail(USV_ERR_ARG, "unknown reset rng");
-  if (kind == USV_RESET_NUMPY_PCG64 && h->cfg.mode != USV_MODE_SIMPLE && h->cfg.mode != USV_MODE_ASMC_SIMPLE)
-    return fail(USV_ERR_ARG, "the NumPy-exact reset exists for usv-simple and usv-asmc-simple only");
   h->sf.np_reset = h->sd.np_reset = kind == USV_RESET_NUMPY_PCG64;
   return USV_OK;
 }

@@ -53,6 +53,16 @@ def np_rng_words(seeds):
     return out.view(np.int32)
 
 
+def np_mt_words(seeds):
+    """USV_FIELD_NP_MT rows: np.random.RandomState(seed)'s MT19937 key[624] and pos, i.e. the
+    global stream after np.random.seed(seed) that the legacy envs' resets draw from."""
+    out = np.zeros((len(seeds), 625), dtype=np.uint32)
+    for i, sd in enumerate(seeds):
+        _, key, pos, _, _ = np.random.RandomState(int(sd)).get_state(legacy=True)
+        out[i, :624], out[i, 624] = key, pos
+    return out.view(np.int32)
+
+
 def _stream_ptr(device):
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
@@ -134,7 +144,10 @@ class UsvVectorEnv:
                     seeds = int(seed) + int(self.cfg.env_id_offset) + np.arange(self.num_envs)
                 else:
                     seeds = np.asarray(seed, dtype=np.int64).reshape(self.num_envs)
-                self.set_field("np_rng", np_rng_words(seeds))
+                if self.env_id in LEGACY_IDS:      # np.random.seed(seed_i) (usv_asmc_env.py:258)
+                    self.set_field("np_mt", np_mt_words(seeds))
+                else:
+                    self.set_field("np_rng", np_rng_words(seeds))
                 self._np_seeded = True
         elif seed is not None:
             _lib.check(self.lib.usv_seed(self._h, ctypes.c_uint64(int(seed))))

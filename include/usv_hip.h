@@ -79,7 +79,8 @@ typedef enum usv_reset_rng {
   USV_RESET_PHILOX = 0,      /* Philox4x32-10 keyed by (seed, global env id, episode): the
                                 reference's reset distributions, not its streams (default)   */
   USV_RESET_NUMPY_PCG64 = 1  /* each env's own numpy Generator(PCG64) (USV_FIELD_NP_RNG), drawn
-                                in the reference's order: resets equal the reference's        */
+                                in the reference's order: resets equal the reference's; the
+                                legacy *-v0 ids draw from np.random's MT19937 (USV_FIELD_NP_MT) */
 } usv_reset_rng;
 
 typedef enum usv_lidar_algo {
@@ -127,6 +128,8 @@ typedef enum usv_field {
                                state high / low and increment high / low 64-bit words as
                                little-endian 32-bit halves, has_uint32, uinteger
                                (bit_generator.state of np.random.PCG64)                    */
+  USV_FIELD_NP_MT,          /* int [625] (legacy *-v0 ids; 0 otherwise): np.random's global
+                               RandomState MT19937 key[624] and pos, for USV_RESET_NUMPY_PCG64 */
   USV_FIELD_COUNT
 } usv_field;
 
@@ -151,8 +154,9 @@ int usv_reward_bytes(void* handle);
 int usv_seed(void* handle, uint64_t seed);
 
 /* Select the reset RNG (usv_reset_rng) <- Env.reset(seed) seeding np_random
- * (simple_env.py:229, gymnasium seeding.np_random); NUMPY_PCG64 for usv-simple and
- * usv-asmc-simple only.  The generator states are set through USV_FIELD_NP_RNG. */
+ * (simple_env.py:229, gymnasium seeding.np_random) and np.random.seed + np.random.uniform
+ * (usv_asmc_env.py:258-279).  The generator states are set through USV_FIELD_NP_RNG /
+ * USV_FIELD_NP_MT. */
 int usv_set_reset_rng(void* handle, int32_t kind);
 
 /* Reset envs whose mask byte is non-zero (all envs if mask_dev == NULL) and write their

@@ -104,3 +104,34 @@ class Pcg64:
                 m = self.next32() * excl
                 left = m & 0xFFFFFFFF
         return lo + (m >> 32)
+
+
+class Mt19937:
+    """np.random's legacy RandomState stream (MT19937) as the legacy envs' resets draw it
+    (np.random.uniform, usv_asmc_env.py:258-279); mirrors the device NpMt."""
+
+    def __init__(self, seed):
+        _, key, pos, _, _ = np.random.RandomState(seed).get_state(legacy=True)
+        self.key, self.pos = [int(k) for k in key], int(pos)
+
+    def _twist(self):
+        k = self.key
+        for i in range(624):
+            y = (k[i] & 0x80000000) | (k[(i + 1) % 624] & 0x7FFFFFFF)
+            k[i] = k[(i + 397) % 624] ^ (y >> 1) ^ (0x9908B0DF if y & 1 else 0)
+        self.pos = 0
+
+    def next32(self):
+        if self.pos >= 624:
+            self._twist()
+        y = self.key[self.pos]
+        self.pos += 1
+        y ^= y >> 11
+        y ^= (y << 7) & 0x9D2C5680
+        y ^= (y << 15) & 0xEFC60000
+        y ^= y >> 18
+        return y & 0xFFFFFFFF
+
+    def uniform(self, lo, hi):
+        a, b = self.next32() >> 5, self.next32() >> 6
+        return lo + (hi - lo) * ((a * 67108864.0 + b) / 9007199254740992.0)

@@ -684,3 +684,37 @@ def test_np_reset_single_env_api(golden):
         if te or tr:
             break
     env.close()
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+@pytest.mark.parametrize("env_id,fname", [("usv-asmc-v0", "asmc_v0_traj.npz"), ("usv-pid-v0", "pid_traj.npz"),
+                                          ("usv-asmc-ye-int-v0", "asmc_ye_int_traj.npz")])
+def test_np_reset_legacy_full_trajectory(golden, env_id, fname, precision):
+    """Legacy ids with reset_rng="numpy": resets draw np.random.uniform from each env's
+    RandomState MT19937 after np.random.seed(seed) (usv_asmc_env.py:258-279), so the reference's
+    rollouts replay whole across their episode ends (reset on done).  f64: usv-pid-v0 /
+    usv-asmc-ye-int-v0 obs bit-identical, usv-asmc-v0 within its float32-rounding tolerance;
+    f32: the first 600 steps."""
+    g = golden(fname)
+    n, T = g["actions"].shape
+    env = make(env_id, n, precision=precision, reset_rng="numpy")
+    obs, _ = env.reset(seed=g["seeds"])
+    (obs,) = to_np(obs)
+    np.testing.assert_allclose(obs, g["obs0"], atol=1e-6 if precision == "f32" else 0, rtol=0)
+    exact = precision == "f64" and env_id != "usv-asmc-v0"
+    tol_o = 0.0 if exact else (5e-6 if precision == "f64" else 2e-3)
+    steps = T if precision == "f64" else 600
+    worst, ends = 0.0, 0
+    for t in range(steps):
+        o, r, te, tr, info = env.step(torch.from_numpy(g["actions"][:, t:t + 1]).cuda())
+        o, r, te, fo = to_np(o, r, te, info["final_obs"])
+        np.testing.assert_array_equal(te, g["done"][:, t], err_msg=f"t={t}")
+        ends += int(te.sum())
+        worst = max(worst, float(np.abs(o - g["obs"][:, t]).max()))
+        if te.any():
+            worst = max(worst, float(np.abs(fo[te] - g["final_obs"][te, t]).max()))
+    print(f"\n[np-reset {env_id} {precision}] {ends} resets over {n}x{steps} steps, max |obs| err {worst:.3e}")
+    assert worst <= tol_o
+    if precision == "f64":
+        assert ends == int(g["done"].sum()) > 0
+    env.close()

@@ -98,3 +98,14 @@ def test_device_reset_draw_order_matches_oracle():
             np.testing.assert_array_equal(orc.ox[i, :k], d["ox"])
             np.testing.assert_array_equal(orc.oy[i, :k], d["oy"])
             np.testing.assert_array_equal(orc.orad[i, :k], d["orad"])
+
+
+@pytest.mark.parametrize("seed", [0, 2000, 4003])
+def test_mt19937_uniform_matches_numpy_random(seed):
+    """The legacy envs' np.random.seed + np.random.uniform stream (usv_asmc_env.py:258-279),
+    across several MT19937 twists."""
+    rs = np.random.RandomState(seed)
+    m = R.Mt19937(seed)
+    for k in range(2000):
+        lo, hi = [(-2.5, 2.5), (-np.pi, np.pi), (15, 30), (0.4, 1.4)][k % 4]
+        assert rs.uniform(lo, hi) == m.uniform(lo, hi), k
