@@ -24,8 +24,8 @@ class _SingleEnv:
 
     def __init__(self, render_mode=None, options=None, device=0, precision="f32",
                  max_episode_steps=0, seed=None, reset_rng="philox"):
-        if render_mode not in (None,):
-            raise NotImplementedError("rendering is out of scope (SURVEY.md §2 #13)")
+        if render_mode not in (None, "rgb_array"):
+            raise NotImplementedError("render_mode 'human' (a pygame window) is out of scope; use 'rgb_array'")
         self.render_mode = render_mode
         self.options = options or {}
         self._venv = UsvVectorEnv(self.env_id, num_envs=1, device=device, precision=precision,
@@ -49,6 +49,12 @@ class _SingleEnv:
         obs, rew, term, trunc, _ = self._venv.step(a)
         return (obs[0].cpu().numpy(), float(rew[0].item()), bool(term[0].item()),
                 bool(trunc[0].item()), {})
+
+    def render(self):
+        """simple_env.py:117-119: an rgb_array frame when render_mode == "rgb_array"."""
+        if self.render_mode == "rgb_array":
+            return self._venv.render(0)
+        return None
 
     def close(self):
         self._venv.close()

@@ -95,7 +95,7 @@ class Sb3VecEnv:
             venv = UsvVectorEnv(env_id, num_envs=num_envs, seed=seed, autoreset=True, **kw)
         self.venv = venv
         self.num_envs = venv.num_envs
-        self.render_mode = None
+        self.render_mode = "rgb_array"               # VecVideoRecorder: env 0 (render.py)
         d = venv.obs_dim
         self._stack = DeviceFrameStack(self.num_envs, d, frame_stack, venv.device) if frame_stack else None
         obs_space = venv.single_observation_space
@@ -180,10 +180,12 @@ class Sb3VecEnv:
         return [False] * len(self._indices(indices))
 
     def get_images(self):
-        raise NotImplementedError("rendering is out of scope (SURVEY.md §2 #13)")
+        """One rgb_array frame per env would copy every env's state off the GPU; like
+        VecVideoRecorder needs, this returns env 0's frame (gym_usv_amd.render)."""
+        return [self.venv.render(0)]
 
     def render(self, mode=None):
-        raise NotImplementedError("rendering is out of scope (SURVEY.md §2 #13)")
+        return self.venv.render(0)
 
     def _indices(self, indices):
         if indices is None:

@@ -208,6 +208,17 @@ class UsvVectorEnv:
                                    dtype=np.int32 if isint else np.float64)
         _lib.check(self.lib.usv_set_field(self._h, f, arr.ctypes.data_as(ctypes.c_void_p), arr.nbytes))
 
+    def render(self, i=0, window_size=512):
+        """rgb_array frame of env i (uint8 [H, W, 3]; gym_usv_amd.render, host-side), for
+        VecVideoRecorder.  usv-simple / usv-asmc-simple only."""
+        from .render import frame_from_state
+        if self.env_id not in ("usv-simple", "usv-asmc-simple"):
+            raise NotImplementedError("the legacy ids' renderer (gym's classic_control viewer) is out of scope")
+        names = ("x", "y", "psi", "path_x0", "path_y0", "path_x1", "path_y1", "progress", "n_obs",
+                 "obs_x", "obs_y", "obs_r")
+        f = {k: self.get_field(k) for k in names}
+        return frame_from_state(f, i, self.obs[i].detach().cpu().numpy(), window_size)
+
     def get_state(self):
         """All per-env state as {field: ndarray} (env checkpoint / parity inspection)."""
         return {k: self.get_field(k) for k in self._fields}
