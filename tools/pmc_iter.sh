@@ -11,7 +11,7 @@ import csv, collections, glob, sys
 for f in sorted(glob.glob("gpurun_out/pmc_*/p*/**/*counter_collection.csv", recursive=True)):
     acc = collections.defaultdict(list)
     for row in csv.DictReader(open(f)):
-        if "step_kernel" in row["Kernel_Name"]:
+        if "step_kernel" in row["Kernel_Name"] or "step_q_kernel" in row["Kernel_Name"]:
             acc[row["Counter_Name"]].append(float(row["Counter_Value"]))
     for k, v in acc.items():
         v = v[5:] or v
