@@ -1,5 +1,6 @@
 # Block-queue step (kind 5) diagnostics: ablation timings (diag/abl_*.so, results not valid) and
-# the per-wave stamp timeline (diag/stamps.so).  Build the libraries on the CPU side first.
+# the per-wave stamp timeline (diag/stamps.so).  Build the libraries on the CPU side first, and take
+# ./diag out of .gpurunignore for the run (it is kept off routine GPU pushes).
 set -e
 cd $GRAFT_REPO_ROOT
 V=${VARIANT:-128,7,5}
