@@ -87,7 +87,18 @@ __device__ __forceinline__ double m_abs(double x) { return fabs(x); }
 
 // Fast paths for the f32 build's per-env scalar math (hardware v_sin/v_cos/v_exp, ~1 ulp at
 // the argument ranges here); the f64 build keeps the correctly rounded libm calls.
-__device__ __forceinline__ void fx_sincos(float x, float* s, float* c) { *s = __sinf(x); *c = __cosf(x); }
+// The heading psi is unwrapped (simple_env.py:323 integrates it without wrapping), so it is first
+// reduced to [-pi, pi] by a two-constant Cody-Waite step: v_sin/v_cos take x / 2pi and lose
+// |x| / 2pi * ulp(1) of absolute accuracy in that product, and leave their domain past 256 turns.
+__device__ __forceinline__ float reduce_2pi(float x) {
+  const float k = rintf(x * 0.159154943f);
+  float r = fmaf(-k, 6.28318548f, x);                 // 2 pi rounded to float (high part)
+  return fmaf(k, 1.74845553e-07f, r);                 // - k (2 pi - that): the low part is < 0
+}
+__device__ __forceinline__ void fx_sincos(float x, float* s, float* c) {
+  const float r = reduce_2pi(x);
+  *s = __sinf(r); *c = __cosf(r);
+}
 __device__ __forceinline__ void fx_sincos(double x, double* s, double* c) { sincos(x, s, c); }
 __device__ __forceinline__ float  fx_exp(float x)  { return __expf(x); }
 __device__ __forceinline__ double fx_exp(double x) { return exp(x); }
@@ -236,9 +247,20 @@ struct Philox {
 // One UsvAsmc.compute substep (usv_asmc.py:56-242, do_perturb = False).  State `s` holds
 // the 16 unique values: psi_d_last, o, o', o'', eta_dot_last[3], upsilon_dot_last[3],
 // e_u_last, Ka_dot_u_last, Ka_dot_psi_last, e_u_int, Ka_u, Ka_psi.
+// do_perturb force of substep `pstep` (usv_asmc.py:184-199): t = perturb_step * integral_step,
+// k = freq * 2 pi, F = (cos(t k), cos(t + k + 10)) * magnitude (the `t + k + 10` is the
+// reference's), rotated as the row vector F @ J(psi).  Evaluated in double in both builds (t k
+// reaches ~1e4 rad within an episode).
+__device__ __forceinline__ void perturb_force(int pstep, double& fx, double& fy) {
+  const double t = (double)pstep * H;
+  const double k = 10.0 * (2.0 * kPi);
+  fx = cos(t * k) * 5.0;
+  fy = cos(t + k + 10.0) * 5.0;
+}
+
 template <typename R>
 __device__ __forceinline__ void asmc_substep(R (&s)[kAsmcN], R a0, R a1, R& x, R& y, R& psi,
-                                             R& u, R& v, R& r) {
+                                             R& u, R& v, R& r, int pstep = 0, bool perturb = false) {
   // f32 build: hardware sqrt / reciprocal / sin / cos and constant reciprocals (the f64 build
   // keeps IEEE division and libm, bit-exact vs the oracle); hypot == sqrt(u^2 + v^2) here
   const R vmag = fx_sqrt(u * u + v * v);
@@ -290,8 +312,18 @@ __device__ __forceinline__ void asmc_substep(R (&s)[kAsmcN], R a0, R a1, R& x, R
   const R d12 = -yr - (R(YRV) * av + R(YRR) * ar);
   const R d21 = -nv - (R(NVV) * av + R(NVR) * ar);
   const R d22 = -nr - (R(NRV) * av + R(NRR) * ar);
-  const R rhs0 = t0 - c02 * r - d00 * u;
-  const R rhs1 = R(0) - c12 * r - (d11 * v + d12 * r);
+  R sp, cp;
+  fx_sincos(psi, &sp, &cp);                                                // J(psi_old) :179
+  R tt0 = t0, tt1 = R(0);
+  if (perturb) {                                                           // T += F @ J (:184-198)
+    double fx, fy;
+    perturb_force(pstep, fx, fy);
+    const R pfx = R(fx), pfy = R(fy);
+    tt0 = t0 + (pfx * cp + pfy * sp);
+    tt1 = R(0) + (pfx * -sp + pfy * cp);
+  }
+  const R rhs0 = tt0 - c02 * r - d00 * u;
+  const R rhs1 = tt1 - c12 * r - (d11 * v + d12 * r);
   const R rhs2 = t2 - (c20 * u + c21 * v) - (d21 * v + d22 * r);
   const R ud = R(MI00) * rhs0;                                             // :226
   const R vd = R(MI11) * rhs1 + R(MI12) * rhs2;
@@ -300,8 +332,6 @@ __device__ __forceinline__ void asmc_substep(R (&s)[kAsmcN], R a0, R a1, R& x, R
   v = R(H) * (vd + s[8]) / R(2) + v;
   r = R(H) * (rd + s[9]) / R(2) + r;
   s[7] = ud; s[8] = vd; s[9] = rd;
-  R sp, cp;
-  fx_sincos(psi, &sp, &cp);                                                // J(psi_old) :179
   const R xd = cp * u - sp * v, yd = sp * u + cp * v, pd = r;              // :233
   x = R(H) * (xd + s[4]) / R(2) + x;                                       // :234
   y = R(H) * (yd + s[5]) / R(2) + y;

@@ -46,28 +46,37 @@ enum IntField { I_NOBS, I_ELAPSED, I_EPISODE, I_SCAN, I_NINT };
 template <typename R> struct State {
   R* freal;                // [F_NREAL][fstride]
   int32_t* fint;           // [I_NINT][fstride]
-  R4<R>* obst;             // [N][cap] (x, y, r, r*r)
+  R* obst;                 // [N][3][ostride]: per env the planes x[ostride], y[ostride], r[ostride]
+                           //   (slots >= n_obs zero); one env's row is 3 * ostride * sizeof(R) bytes
   R* sensor_last;          // [N][128]
   R* asmc;                 // [16][N]
   R* v0;                   // [21][fstride] legacy envs: last[9], aux[3], target[6], action_last,
                            //   ye_int, ye_last (usv-asmc-ye-int-v0)
   const R* ray_tab;        // [128][2] (cos, sin)(start + i*res)
-  R4<R>* pose;             // [N][2] pose record after the step's dynamics (split step):
+  R4<R>* pose;             // [N][2] pose record after the step's dynamics (split wave step):
                            //   (x, y, sin psi, cos psi), (partial reward, n_obs, truncated, 0)
+  float* qrec;             // [N][kQRec] f32 env record of the split block-queue step (dyn_rec_kernel)
   uint32_t* nprng;         // [10][fstride] NumPy PCG64 per env (state hi/lo, inc hi/lo as 32-bit
                            //   words, has_uint32, uinteger) for the NumPy-exact reset
   uint32_t* npmt;          // [625][fstride] legacy envs: np.random.RandomState MT19937 key[624], pos
   int np_reset;            // 1: resets draw from NumPy's Generator(PCG64) (np_reset) -- legacy
                            //   envs: from np.random's MT19937 (NpMt) -- not Philox
+  int perturb;             // usv-asmc-simple: do_perturb (USV_FLAG_PERTURB)
+  const R* exp;            // custom experiment applied by every reset, or null (kExp* layout)
   int N, cap, limit, autoreset;
   int prio;                // scan loops: raise the issue priority of lagging waves (s_setprio)
   int fstride;             // elements between fields (>= N, 256-B aligned)
+  int ostride;             // obstacle plane stride: cap rounded up to a multiple of 4
   uint64_t seed, gid0;
   __host__ __device__ R* F(int i) const { return freal + (size_t)i * fstride; }
   __host__ __device__ int32_t* I(int i) const { return fint + (size_t)i * fstride; }
   __host__ __device__ R* V(int i) const { return v0 + (size_t)i * fstride; }
+  __host__ __device__ R* orow(int e) const { return obst + (size_t)e * 3 * ostride; }
 };
 constexpr int kV0Last = 0, kV0Aux = 9, kV0Target = 12, kV0ALast = 18, kV0Ye = 19, kV0N = 21;
+// custom experiment record (usv_experiment, simple_env.py:292-300), in R: n, path start (2),
+// path angle, pose (3), pad, then x[cap], y[cap], r[cap]
+constexpr int kExpN = 0, kExpPS = 1, kExpAngle = 3, kExpPose = 4, kExpObs = 8;
 
 template <typename R> struct IO {
   const float* act;        // [N][2]
@@ -77,6 +86,8 @@ template <typename R> struct IO {
   uint8_t* trunc;          // [N]
   float* fobs;             // [N][143] or null
   const uint8_t* mask;     // [N] or null (reset kernel)
+  float* info;             // [N][USV_INFO_DIM] or null: step info (step kernels) / reset info
+  int kpath;               // reset kernel: options['place_obstacles_on_path'] (0 = none)
 };
 
 constexpr int kBlock = 256;
@@ -207,8 +218,76 @@ __device__ __forceinline__ void philox_uniforms(Philox& g, int l, Uni4<double>& 
   o.u[3] = (double)((((uint64_t)b[2] << 32) | b[3]) >> 11) * k;
 }
 
+// Reset info row _get_info(-1, zeros(3)) (simple_env.py:102-115, :305); reward terms 0.
+template <typename R>
+__device__ __forceinline__ void reset_info(float* info, R x, R y, R psi, R u, R v, R r, R px0, R py0,
+                                           R px1, R py1, R ye, float angle_n) {
+  const float vals[USV_INFO_DIM] = {(float)x, (float)y, (float)psi, (float)u, (float)v, (float)r,
+                                    (float)px0, (float)py0, (float)px1, (float)py1, 0.0f, 0.0f,
+                                    (float)ye, angle_n, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+  for (int i = 0; i < USV_INFO_DIM; ++i) info[i] = vals[i];
+}
+
+// cross-track error of (x, y) w.r.t. the path (simple_env.py:133-137); sin/cos of the path angle
+// a_k = atan2(dy, dx) are dy/|d| and dx/|d|
+template <typename R>
+__device__ __forceinline__ R path_ye(R x, R y, R x0, R y0, R x1, R y1) {
+  const R dx = x1 - x0, dy = y1 - y0;
+  const R inv_len = R(1) / m_sqrt(dx * dx + dy * dy);
+  return -(x - x0) * (dy * inv_len) + (y - y0) * (dx * inv_len);
+}
+
+// run_custom_experiment (simple_env.py:292-300): after the usual draws of a reset, the drawn
+// obstacles, path and pose are replaced by the experiment's; target, velocity and action limits
+// stay drawn.  One lane per env: it re-derives the drawn scalars of episode `ep` from their Philox
+// lanes (33..35 of reset_wave), then rewrites obstacles, state, the obs header and info.  Run by
+// the reset kernel after reset_wave and, for same-step autoresets, by exp_autoreset_kernel after
+// the step (kept out of the step kernels, whose pair loop it would make spill).
+template <typename R>
+__device__ __forceinline__ void reset_experiment(const State<R>& S, int e, int ep, float* row, float* info) {
+  const R* X = S.exp;
+  R tx, ty, u, v, r, mu, mr, refv;
+  {
+    Philox g(S.seed, S.gid0 + (uint64_t)e, (uint32_t)ep);
+    Uni4<R> U33, U34, U35;
+    philox_uniforms(g, 33, U33);
+    philox_uniforms(g, 34, U34);
+    philox_uniforms(g, 35, U35);
+    tx = R(kBound) * U33.u[1]; ty = R(kBound) * U33.u[2];
+    u = R(0.15) * U33.u[3]; v = R(0.15) * U34.u[0]; r = R(0.15) * U34.u[1];
+    mu = R(1.5) + R(1.5) * U34.u[2];
+    mr = R(3) + R(3) * U34.u[3];
+    refv = R(0.75) + (mu - R(0.75)) * U35.u[0];
+  }
+  const int cnt = (int)X[kExpN];
+  R* ob = S.orow(e);
+  for (int j = 0; j < S.cap; ++j) {
+    ob[j] = j < cnt ? X[kExpObs + j] : R(0);
+    ob[S.ostride + j] = j < cnt ? X[kExpObs + S.cap + j] : R(0);
+    ob[2 * S.ostride + j] = j < cnt ? X[kExpObs + 2 * S.cap + j] : R(0);
+  }
+  const R ps0 = X[kExpPS], ps1 = X[kExpPS + 1];
+  R sx2, cx2;
+  m_sincos(X[kExpAngle], &sx2, &cx2);
+  const R pe0 = ps0 + cx2 * R(100), pe1 = ps1 + sx2 * R(100);                     // :296
+  const R px = X[kExpPose], py = X[kExpPose + 1], psi = X[kExpPose + 2];
+  S.F(F_X)[e] = px; S.F(F_Y)[e] = py; S.F(F_PSI)[e] = psi;
+  S.F(F_PX0)[e] = ps0; S.F(F_PY0)[e] = ps1;
+  S.F(F_PX1)[e] = pe0; S.F(F_PY1)[e] = pe1;
+  S.I(I_NOBS)[e] = cnt;
+  const R angle = wrap_angle(m_atan2(ty - py, tx - px) - psi);                    // :302, :63-80
+  const R dst = m_hypot(px - tx, py - ty);
+  const R ye = path_ye(px, py, ps0, ps1, pe0, pe1);
+  float h[kHdr];
+  make_header<R>(h, u, v, r, angle, dst, ye, refv, R(0), R(0), mu, mr);
+  for (int i = 0; i < kHdr; ++i) row[i] = h[i];
+  if (info) reset_info<R>(info, px, py, psi, u, v, r, ps0, ps1, pe0, pe1, ye, h[3]);
+}
+
 template <typename R, int MODE>
-__device__ __forceinline__ void reset_wave(const State<R>& S, int e, float* row) {
+__device__ __forceinline__ void reset_wave(const State<R>& S, int e, float* row, float* info = nullptr,
+                                           int kpath = 0) {
   if (S.np_reset) return;                  // NumPy-exact mode: np_autoreset_kernel resets after the step
   const int l = lane_id();
   const int ep = uniform(S.I(I_EPISODE)[e]);
@@ -235,18 +314,37 @@ __device__ __forceinline__ void reset_wave(const State<R>& S, int e, float* row)
   const unsigned long long ball = ballot(keep);
   int cnt = __popcll(ball);
   const int pos = __builtin_amdgcn_mbcnt_hi((unsigned)(ball >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)ball, 0));
-  R4<R>* ob = S.obst + (size_t)e * S.cap;
-  if (keep) ob[pos] = R4<R>{ox, oy, orad, orad * orad};
+  R* ob = S.orow(e);
+  const int os = S.ostride;
+  if (keep) { ob[pos] = ox; ob[os + pos] = oy; ob[2 * os + pos] = orad; }
   if (cnt == 0) {
     const R fx = R(kBound) * bcast(U.u[2], 35), fy = R(kBound) * bcast(U.u[3], 35);
     const R fr = R(0.15) + R(0.35) * bcast(U.u[0], 36);
-    if (l == 0) ob[0] = R4<R>{fx, fy, fr, fr * fr};
+    if (l == 0) { ob[0] = fx; ob[os] = fy; ob[2 * os] = fr; }
     cnt = 1;
   }
-  if (l >= cnt && l < S.cap) ob[l] = R4<R>{R(0), R(0), R(0), R(0)};
+  const R ang = R(-kPi) + R(2 * kPi) * bcast(U.u[3], 32);
+  if (kpath > 0) {
+    // options['place_obstacles_on_path'] (:276-288): k obstacles at N(path_start + (cos, sin)(angle)
+    // * U(0, hypot(0, 20) = 20), 1) per axis, appended unfiltered; lane j draws obstacle j from the
+    // Philox block at counter j + 128 (explicit resets only: the step kernels pass kpath = 0)
+    R sa, ca;
+    m_sincos(ang, &sa, &ca);
+    Uni4<R> P;
+    philox_uniforms(g, l + 128, P);
+    const R mag = R(kBound) * P.u[0];
+    const R bq = m_sqrt(R(-2) * log(R(1) - P.u[1]));
+    R s2, c2;
+    m_sincos(R(2 * kPi) * P.u[2], &s2, &c2);
+    const R lx = (ca * mag + sx) + bq * c2, ly = (sa * mag + sy) + bq * s2;
+    const R lr = R(0.15) + R(0.35) * P.u[3];
+    if (l < kpath) { ob[cnt + l] = lx; ob[os + cnt + l] = ly; ob[2 * os + cnt + l] = lr; }
+    cnt += kpath;
+  }
+  if (l >= cnt && l < S.cap) { ob[l] = R(0); ob[os + l] = R(0); ob[2 * os + l] = R(0); }
   if (MODE == USV_MODE_ASMC_SIMPLE && l < kAsmcN) S.asmc[(size_t)l * S.N + e] = R(0);  // simple_env_asmc.py:15
   if (l == 0) {
-    const R psi = R(-kPi) + R(2 * kPi) * bcast(U.u[2], 32), ang = R(-kPi) + R(2 * kPi) * bcast(U.u[3], 32);
+    const R psi = R(-kPi) + R(2 * kPi) * bcast(U.u[2], 32);
     const R dist = R(100) + R(10) * bcast(U.u[0], 33);
     const R u = R(0.15) * bcast(U.u[3], 33), v = R(0.15) * bcast(U.u[0], 34), r = R(0.15) * bcast(U.u[1], 34);
     const R mr = R(3) + R(3) * bcast(U.u[3], 34);
@@ -271,6 +369,7 @@ __device__ __forceinline__ void reset_wave(const State<R>& S, int e, float* row)
     make_header<R>(h, u, v, r, angle, dst, R(0), refv, R(0), R(0), mu, mr);
 #pragma unroll
     for (int i = 0; i < kHdr; ++i) row[i] = h[i];
+    if (info) reset_info<R>(info, sx, sy, psi, u, v, r, sx, sy, sx + ca * dist, sy + sa * dist, R(0), h[3]);
   }
 }
 
@@ -359,7 +458,7 @@ __device__ __forceinline__ void np_store(const State<R>& S, int e, const NpPcg64
 // zeroes the ASMC state (simple_env_asmc.py:14-16).  Writes the reset obs header into `row`
 // (its sensor half, the stale scan, is the caller's).  Draws in double, stored as R.
 template <typename R, int MODE>
-__device__ void np_reset(const State<R>& S, int e, float* row) {
+__device__ void np_reset(const State<R>& S, int e, float* row, float* info = nullptr, int kpath = 0) {
   NpPcg64 g = np_load(S, e);
   const double sx = 0.5 * g.standard_normal() + kBound / 2;                      // :234-235
   const double sy = 0.5 * g.standard_normal() + kBound / 2;
@@ -373,31 +472,52 @@ __device__ void np_reset(const State<R>& S, int e, float* row) {
   const double mr = g.uniform(3, 6);                                             // :250
   const double refv = g.uniform(0.75, mu);                                       // :251
   const int n = g.integers(15, 30);                                              // :257
-  R4<R>* ob = S.obst + (size_t)e * S.cap;
+  R* ob = S.orow(e);
+  const int os = S.ostride;
   int cnt = 0;
   for (int j = 0; j < n; ++j) {                                                  // :258-268
     const double ox = g.uniform(0, kBound), oy = g.uniform(0, kBound);
-    if (!(hypot(sx - ox, sy - oy) < 0.5 || hypot(tx - ox, ty - oy) < 0.5)) ob[cnt++] = R4<R>{R(ox), R(oy), R(0), R(0)};
+    if (!(hypot(sx - ox, sy - oy) < 0.5 || hypot(tx - ox, ty - oy) < 0.5)) {
+      ob[cnt] = R(ox); ob[os + cnt] = R(oy); ++cnt;
+    }
   }
   if (cnt == 0) {                                                                // :270-274
     const double ox = g.uniform(0, kBound), oy = g.uniform(0, kBound);
-    ob[cnt++] = R4<R>{R(ox), R(oy), R(0), R(0)};
+    ob[0] = R(ox); ob[os] = R(oy); cnt = 1;
   }
-  for (int j = 0; j < cnt; ++j) {                                                // :290
-    const R rad = R(g.uniform(0.15, 0.5));
-    ob[j].z = rad;
-    ob[j].w = rad * rad;
+  if (kpath > 0) {                                                               // :276-288
+    // mag = uniform(0, hypot(*env_bounds) = hypot(0, 20), k); line_x = normal(cos(angle) * mag +
+    // path_start[0], 1); line_y likewise: k uniforms, then k normals per axis
+    // (the k magnitudes are re-drawn from copies of the generator instead of being buffered)
+    const double ca = cos(ang), sa = sin(ang);
+    NpPcg64 gx = g, gy = g;
+    for (int j = 0; j < kpath; ++j) (void)g.next_double();
+    for (int j = 0; j < kpath; ++j) ob[cnt + j] = R((ca * gx.uniform(0, kBound) + sx) + g.standard_normal());
+    for (int j = 0; j < kpath; ++j) ob[os + cnt + j] = R((sa * gy.uniform(0, kBound) + sy) + g.standard_normal());
+    cnt += kpath;
   }
-  for (int j = cnt; j < S.cap; ++j) ob[j] = R4<R>{R(0), R(0), R(0), R(0)};
+  for (int j = 0; j < cnt; ++j) ob[2 * os + j] = R(g.uniform(0.15, 0.5));      // :290
   np_store(S, e, g);
+  double ps0 = sx, ps1 = sy, pe0 = sx + cos(ang) * dist, pe1 = sy + sin(ang) * dist;   // :243
+  double px = sx, py = sy, pp = psi;
+  if (const R* X = S.exp) {                                                      // :292-300
+    cnt = (int)X[kExpN];
+    for (int j = 0; j < cnt; ++j) {
+      ob[j] = X[kExpObs + j]; ob[os + j] = X[kExpObs + S.cap + j]; ob[2 * os + j] = X[kExpObs + 2 * S.cap + j];
+    }
+    ps0 = (double)X[kExpPS]; ps1 = (double)X[kExpPS + 1];
+    pe0 = ps0 + cos((double)X[kExpAngle]) * 100; pe1 = ps1 + sin((double)X[kExpAngle]) * 100;
+    px = (double)X[kExpPose]; py = (double)X[kExpPose + 1]; pp = (double)X[kExpPose + 2];
+  }
+  for (int j = cnt; j < S.cap; ++j) { ob[j] = R(0); ob[os + j] = R(0); ob[2 * os + j] = R(0); }
   if (MODE == USV_MODE_ASMC_SIMPLE)
     for (int i = 0; i < kAsmcN; ++i) S.asmc[(size_t)i * S.N + e] = R(0);
-  const R x0 = R(sx), y0 = R(sy), ps = R(psi);
+  const R x0 = R(px), y0 = R(py), ps = R(pp);
   S.F(F_X)[e] = x0; S.F(F_Y)[e] = y0; S.F(F_PSI)[e] = ps;
   S.F(F_U)[e] = R(u); S.F(F_V)[e] = R(v); S.F(F_R)[e] = R(r);
   S.F(F_PROGRESS)[e] = R(0);
-  S.F(F_PX0)[e] = x0; S.F(F_PY0)[e] = y0;
-  S.F(F_PX1)[e] = R(sx + cos(ang) * dist); S.F(F_PY1)[e] = R(sy + sin(ang) * dist);   // :243
+  S.F(F_PX0)[e] = R(ps0); S.F(F_PY0)[e] = R(ps1);
+  S.F(F_PX1)[e] = R(pe0); S.F(F_PY1)[e] = R(pe1);
   S.F(F_MAX_U)[e] = R(mu); S.F(F_MAX_R)[e] = R(mr); S.F(F_REF_V)[e] = R(refv);
   S.I(I_NOBS)[e] = cnt;
   S.I(I_ELAPSED)[e] = 0;
@@ -405,9 +525,11 @@ __device__ void np_reset(const State<R>& S, int e, float* row) {
   S.I(I_SCAN)[e] = 0;
   const R angle = wrap_angle(m_atan2(R(ty) - y0, R(tx) - x0) - ps);             // :302, :63-80
   const R dst = m_hypot(x0 - R(tx), y0 - R(ty));
+  const R ye = S.exp ? path_ye(x0, y0, R(ps0), R(ps1), R(pe0), R(pe1)) : R(0);
   float h[kHdr];
-  make_header<R>(h, R(u), R(v), R(r), angle, dst, R(0), R(refv), R(0), R(0), R(mu), R(mr));
+  make_header<R>(h, R(u), R(v), R(r), angle, dst, ye, R(refv), R(0), R(0), R(mu), R(mr));
   for (int i = 0; i < kHdr; ++i) row[i] = h[i];
+  if (info) reset_info<R>(info, x0, y0, ps, R(u), R(v), R(r), R(ps0), R(ps1), R(pe0), R(pe1), ye, h[3]);
 }
 
 // Same-step autoreset in NumPy-exact mode, after the step kernel: envs that ended this step get
@@ -419,21 +541,33 @@ __global__ __launch_bounds__(kBlock) void np_autoreset_kernel(State<R> S, IO<R> 
   np_reset<R, MODE>(S, e, io.obs + (size_t)e * kObsDim);
 }
 
+// Same-step autoreset with a custom experiment installed (Philox resets): after the step kernel,
+// envs that ended this step get the experiment's obstacles, path and pose (simple_env.py:292-300).
+template <typename R>
+__global__ __launch_bounds__(kBlock) void exp_autoreset_kernel(State<R> S, IO<R> io) {
+  const int e = blockIdx.x * kBlock + threadIdx.x;
+  if (e >= S.N || !(io.term[e] | io.trunc[e])) return;
+  reset_experiment<R>(S, e, S.I(I_EPISODE)[e] - 1, io.obs + (size_t)e * kObsDim, nullptr);
+}
+
 // --------------------------------------------------------------------------- phase 1
 // UsvSimpleEnv.step kinematics..reward terms (simple_env.py:310-346); for usv-asmc-simple
 // first 2x UsvAsmc.compute (simple_env_asmc.py:18-27) and then step(zeros(2)).
 // Also returns sin/cos of the new heading so the wave-per-env lidar does not recompute them.
 template <typename R, int MODE>
 __device__ void env_dynamics(const State<R>& S, int e, float a_u, float a_r, float (&hdr)[kHdr],
-                             R& px, R& py, R& psp, R& pcp, R& partial, bool& trunc) {
+                             R& px, R& py, R& psp, R& pcp, R& partial, bool& trunc, float* info = nullptr) {
   R x = S.F(F_X)[e], y = S.F(F_Y)[e], psi = S.F(F_PSI)[e];
   R u = S.F(F_U)[e], v = S.F(F_V)[e], r = S.F(F_R)[e];
+  const int el0 = S.I(I_ELAPSED)[e];
   if (MODE == USV_MODE_ASMC_SIMPLE) {
     R s[kAsmcN];
 #pragma unroll
     for (int i = 0; i < kAsmcN; ++i) s[i] = S.asmc[(size_t)i * S.N + e];
     const R c0 = R(a_u), c1 = R(a_r);
-    for (int k = 0; k < 20; ++k) asmc_substep<R>(s, c0, c1, x, y, psi, u, v, r);
+    // perturb_step of the episode's UsvAsmc: 2 compute() x 10 substeps per env step (usv_asmc.py:199)
+    const bool pert = S.perturb != 0;
+    for (int k = 0; k < 20; ++k) asmc_substep<R>(s, c0, c1, x, y, psi, u, v, r, 20 * el0 + k, pert);
 #pragma unroll
     for (int i = 0; i < kAsmcN; ++i) S.asmc[(size_t)i * S.N + e] = s[i];
     a_u = 0.0f;                                                                   // step(zeros(2))
@@ -471,7 +605,7 @@ __device__ void env_dynamics(const State<R>& S, int e, float a_u, float a_r, flo
   const R angle = wrap_angle(m_atan2(ty - y, tx - x) - psi);
   const R ddx = x - tx, ddy = y - ty;
   const R dist = m_sqrt(ddx * ddx + ddy * ddy);
-  const int el = S.I(I_ELAPSED)[e] + 1;
+  const int el = el0 + 1;
   trunc = (x > R(kBound)) | (x < R(0)) | (y > R(kBound)) | (y < R(0)) |   // :336
           (S.limit > 0 && el >= S.limit);                                 // TimeLimit
   make_header<R>(hdr, u, v, r, angle, dist, ye, refv, lu, lr, mu, mr);   // obs uses PREVIOUS action
@@ -484,6 +618,15 @@ __device__ void env_dynamics(const State<R>& S, int e, float a_u, float a_r, flo
   const R vel_r = fx_exp(-m_abs(m_sqrt(u * u + v * v) - refv)) * R(0.05);
   const R dact_r = -(dact / R(2)) * R(0.15);
   partial = ye_r + ang_r + vel_r + dact_r;
+  if (info) {                                        // _get_info + reward_info (:102-115, :189-199)
+    const float vals[USV_INFO_DIM] = {
+        (float)x, (float)y, (float)psi, (float)u, (float)v, (float)r, (float)x0, (float)y0,
+        (float)S.F(F_PX1)[e], (float)S.F(F_PY1)[e], (float)a3u, (float)a3r, (float)ye, hdr[3],
+        (float)ye_r, (float)ang_r, (float)dact_r, (float)dact, (float)vel_r, (float)refv, (float)lu,
+        (float)(lu - refv)};
+#pragma unroll
+    for (int i = 0; i < USV_INFO_DIM; ++i) info[i] = vals[i];
+  }
   S.F(F_X)[e] = x; S.F(F_Y)[e] = y; S.F(F_PSI)[e] = psi;
   S.F(F_U)[e] = u; S.F(F_V)[e] = v; S.F(F_R)[e] = r;
   S.F(F_LAST_U)[e] = a3u; S.F(F_LAST_R)[e] = a3r;
@@ -664,17 +807,11 @@ struct WinLds {
   const float2* rayoff;       // [128] block-shared ray offset table
 };
 
-// One env's obstacle row in LDS: SoA planes (block kernel, staged through registers) or the
-// global AoS (x, y, r, r^2) row copied verbatim by LDS-DMA (wave kernel).
+// One env's obstacle row in LDS: the x, y, r planes (the global row copied verbatim by LDS-DMA,
+// or staged through registers by the reset kernel).
 template <typename R> struct RowSoA {
   const R* x; const R* y; const R* r;
   __device__ __forceinline__ void get(int j, R& X, R& Y, R& Rr) const { X = x[j]; Y = y[j]; Rr = r[j]; }
-};
-template <typename R> struct RowAoS {
-  const R4<R>* p;
-  __device__ __forceinline__ void get(int j, R& X, R& Y, R& Rr) const {
-    const R4<R> v = p[j]; X = v.x; Y = v.y; Rr = v.z;
-  }
 };
 
 // Inclusive max-scan over the 64 lanes of non-negative values (DPP row scans + row_bcast
@@ -767,18 +904,16 @@ __device__ __forceinline__ void lidar_window(float dx, float dy, float key, floa
 // and each pair takes the pose of its owner's env.  The per-obstacle setup, the scans and the
 // pass overhead are shared by the two envs; each pair runs the identical exact test, so the
 // readings are bit-identical to one-env-per-wave.  Slots [256]: env A rays, then env B rays.
-struct Pose2 { float pxA, pyA, spA, cpA, pxB, pyB, spB, cpB; };    // wave-uniform
-
+//
 // The obstacle lanes leave (a, b, r^2, key bits) records in the rows buffer (lane j at slot j;
-// each lane overwrites only what one ds instruction of this wave has already read), and each
-// pair reads its owner's record: no pose select, no rotation and no re-read of the row per pair.
+// written after every lane's row reads, which the wave's LDS instructions complete in order),
+// and each pair reads its owner's record: no pose select, no rotation and no re-read of the row.
+// Each lane brings its own env's ray-0 direction (c0r, s0r) = (cos, sin)(psi - 120 deg).
 template <bool RANGE_CHECK>
 __device__ __forceinline__ void lidar_window2(float dx, float dy, float key, float d, float rr, bool valid,
-                                              float sp, float cp, float4* rec, const WinLds& L,
+                                              float c0r, float s0r, float4* rec, const WinLds& L,
                                               Scan<float>& A, Scan<float>& B) {
   const int l = lane_id();
-  const float c0r = ray_c(cp, sp, (float)kStartC, (float)kStartS);
-  const float s0r = ray_s(cp, sp, (float)kStartC, (float)kStartS);
   float a, b;
   to_ray0(dx, dy, c0r, s0r, a, b);
   const float phi = fast_atan2(b, a);                 // CCW angle from ray 0; ray i at i*res
@@ -836,18 +971,18 @@ __device__ __forceinline__ void lidar_window2(float dx, float dy, float key, flo
   B.rd1 = b1s != ~0ull ? __uint_as_float((unsigned)b1s) : (float)kSensorMax;
 }
 
-// rows: LDS, env A's row at [0, cap), env B's at [cap, 2 cap); nB = 0 when there is no env B.
-__device__ __forceinline__ void lidar_wave2(float4* rows, int cap, int nA, int nB, const Pose2& P,
-                                            const float2* rayoff, unsigned long long* slot, int* mark,
-                                            Scan<float>& A, Scan<float>& B) {
+// rows: LDS buffer (>= 1 KiB, reused for the per-obstacle records) holding env A's obstacle row
+// (planes x, y, r of stride os) at rows[0] and env B's at rows[3 os].  Per lane: its env's pose
+// (px, py), ray-0 direction (c0r, s0r) and obstacle count nl (0: no env in this half).
+__device__ __forceinline__ void lidar_wave2(float* rows, int os, int nl, float px, float py, float c0r,
+                                            float s0r, const float2* rayoff, unsigned long long* slot,
+                                            int* mark, Scan<float>& A, Scan<float>& B) {
   const int l = lane_id();
-  const bool hb = l >= 32;
   const int jl = l & 31;
-  const bool valid = jl < (hb ? nB : nA);
-  const float px = hb ? P.pxB : P.pxA, py = hb ? P.pyB : P.pyA;
-  const float sp = hb ? P.spB : P.spA, cp = hb ? P.cpB : P.cpA;
+  const bool valid = jl < nl;
+  const float* rb = rows + (l >= 32 ? 3 * os : 0);
   float ox = 0.0f, oy = 0.0f, rr = 0.0f;
-  if (valid) { const float4 o = rows[(hb ? cap : 0) + jl]; ox = o.x; oy = o.y; rr = o.z; }
+  if (valid) { ox = rb[jl]; oy = rb[os + jl]; rr = rb[2 * os + jl]; }
   const float dx = ox - px, dy = oy - py;
   const float d = l_sqrt(m_fma(dx, dx, dy * dy));
   const float key = valid ? d - rr : big<float>();                              // simple_env.py:205-206
@@ -856,8 +991,8 @@ __device__ __forceinline__ void lidar_wave2(float4* rows, int cap, int nA, int n
   A.far = B.far = false;
   const bool far = ballot(valid & (d >= (float)(0.99 * kSensorMax))) != 0;
   const WinLds W{slot, mark, rayoff};
-  if (!far) lidar_window2<false>(dx, dy, key, d, rr, valid, sp, cp, rows, W, A, B);
-  else lidar_window2<true>(dx, dy, key, d, rr, valid, sp, cp, rows, W, A, B);
+  if (!far) lidar_window2<false>(dx, dy, key, d, rr, valid, c0r, s0r, reinterpret_cast<float4*>(rows), W, A, B);
+  else lidar_window2<true>(dx, dy, key, d, rr, valid, c0r, s0r, reinterpret_cast<float4*>(rows), W, A, B);
 }
 
 template <typename R, int LID, typename Row>
@@ -884,23 +1019,14 @@ __device__ __forceinline__ void lidar_wave(const Row& E, int n, R px, R py, R sp
                                                   t0.x, t0.y, t1.x, t1.y, out);
 }
 
-template <typename R, int EPB> struct alignas(16) Scratch {
-  R px[EPB], py[EPB], sp[EPB], cp[EPB], partial[EPB];
-  int n[EPB];
-  uint8_t trunc[EPB], term[EPB], coll[EPB];
-};
-
-// Dynamic LDS carve (16-B aligned pieces):
+// Reset-kernel LDS carve (16-B aligned pieces):
 //   [ray offset table 128 x Vec2][pair slots 4 waves x 128 x u64][owner marks 4 x 64 x i32]
-//   [obstacle rows: x[EPB][cap], y[EPB][cap], r[EPB][cap]]
+//   [one obstacle row per wave: x[64], y[64], r[64]]
 template <typename R> __host__ __device__ constexpr size_t lds_rayoff_bytes() { return 128 * 2 * sizeof(R); }
 constexpr size_t kLdsSlotBytes = (size_t)kWaves * 128 * 8;
 constexpr size_t kLdsMarkBytes = (size_t)kWaves * 64 * 4;
 template <typename R> __host__ __device__ constexpr size_t lds_head_bytes() {
   return lds_rayoff_bytes<R>() + kLdsSlotBytes + kLdsMarkBytes;
-}
-template <typename R> __host__ __device__ size_t lds_bytes(int epb, int cap) {
-  return lds_head_bytes<R>() + 3 * (((size_t)epb * cap * sizeof(R) + 15) & ~(size_t)15);
 }
 
 // Block prologue shared by the step and reset kernels: ray-offset table and slot init.
@@ -912,131 +1038,6 @@ __device__ __forceinline__ void lds_prologue(const State<R>& S, char* lds, int t
   for (int i = tid; i < kWaves * 128; i += kBlock) slots[i] = ~0ull;
 }
 
-// --------------------------------------------------------------------------- step kernel
-template <typename R, int MODE, int EPB, int LID>
-__device__ __forceinline__ void step_body(const State<R>& S, const IO<R>& io) {
-  __shared__ Scratch<R, EPB> sh;
-  extern __shared__ __attribute__((aligned(16))) char lds[];
-  auto* rayoff = reinterpret_cast<typename Vec2<R>::T*>(lds);
-  auto* slots = reinterpret_cast<unsigned long long*>(lds + lds_rayoff_bytes<R>());
-  int* marks = reinterpret_cast<int*>(lds + lds_rayoff_bytes<R>() + kLdsSlotBytes);
-  const int tid = threadIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(tid / kWave);   // wave-uniform (SGPR)
-  const int l = lane_id();
-  const int e0 = blockIdx.x * EPB;
-  const int ne = S.N - e0 < EPB ? S.N - e0 : EPB;   // envs of this block
-  const int cap = S.cap;
-  const size_t plane = (((size_t)EPB * cap * sizeof(R) + 15) & ~(size_t)15) / sizeof(R);
-  R* lox = reinterpret_cast<R*>(lds + lds_head_bytes<R>());
-  R* loy = lox + plane;
-  R* lor = loy + plane;
-
-  USV_STAMP(0);
-  lds_prologue(S, lds, tid);
-  // The dynamics wave rotates with the block index: the dispatcher places wave w of every block
-  // on SIMD w, so a fixed wave 0 would put all resident blocks' phase 1 on one SIMD.
-  const int dw = blockIdx.x & (kWaves - 1);
-  if (wave == dw) {
-    // ---- phase 1 (one wave): lane-per-env dynamics; the obs header goes straight to the row
-    if (l < ne) {
-      const int e = e0 + l;
-      const float2 a = reinterpret_cast<const float2*>(io.act)[e];
-      float hdr[kHdr];
-      R px, py, sp, cp, partial;
-      bool trunc;
-#ifdef USV_DIAG_NODYN
-      px = S.F(F_X)[e] + a.x; py = S.F(F_Y)[e] + a.y; sp = R(0.5); cp = R(0.8); partial = R(0); trunc = false;
-      for (int i = 0; i < kHdr; ++i) hdr[i] = (float)px;
-#else
-      env_dynamics<R, MODE>(S, e, a.x, a.y, hdr, px, py, sp, cp, partial, trunc);
-#endif
-      float* row = io.obs + (size_t)e * kObsDim;
-#pragma unroll
-      for (int i = 0; i < kHdr; ++i) row[i] = hdr[i];
-      sh.px[l] = px; sh.py[l] = py; sh.sp[l] = sp; sh.cp[l] = cp;
-      sh.partial[l] = partial;
-      sh.trunc[l] = trunc;
-      sh.n[l] = S.I(I_NOBS)[e];
-    }
-    USV_STAMP_B(1);
-  } else {
-    // ---- phase 1 (the other three waves): stage this block's obstacle rows in LDS (SoA)
-    // meanwhile; staging wave sw = 0..2 takes rows sw, sw+3, ...; four loads in flight
-    const int sw = (wave - dw - 1) & (kWaves - 1);
-    const R4<R>* src = S.obst + (size_t)e0 * cap + l;
-    const R4<R> z{R(0), R(0), R(0), R(0)};
-    const bool lane_ok = l < cap;
-    for (int k = sw; k < ne; k += 4 * (kWaves - 1)) {
-      const int k1 = k + (kWaves - 1), k2 = k + 2 * (kWaves - 1), k3 = k + 3 * (kWaves - 1);
-      const R4<R> b0 = lane_ok ? src[(size_t)k * cap] : z;
-      const R4<R> b1 = lane_ok && k1 < ne ? src[(size_t)k1 * cap] : z;
-      const R4<R> b2 = lane_ok && k2 < ne ? src[(size_t)k2 * cap] : z;
-      const R4<R> b3 = lane_ok && k3 < ne ? src[(size_t)k3 * cap] : z;
-      if (lane_ok) {
-        lox[k * cap + l] = b0.x; loy[k * cap + l] = b0.y; lor[k * cap + l] = b0.z;
-        if (k1 < ne) { lox[k1 * cap + l] = b1.x; loy[k1 * cap + l] = b1.y; lor[k1 * cap + l] = b1.z; }
-        if (k2 < ne) { lox[k2 * cap + l] = b2.x; loy[k2 * cap + l] = b2.y; lor[k2 * cap + l] = b2.z; }
-        if (k3 < ne) { lox[k3 * cap + l] = b3.x; loy[k3 * cap + l] = b3.y; lor[k3 * cap + l] = b3.z; }
-      }
-    }
-  }
-  __syncthreads();
-  USV_STAMP(2);
-
-  // ---- phase 2: wave-per-env lidar + observation rows
-  unsigned long long* wslot = slots + wave * 128;
-  int* wmark = marks + wave * 64;
-  for (int k = wave; k < ne; k += kWaves) {
-    const int e = e0 + k;
-    const int n = uniform(sh.n[k]);
-    Scan<R> sc;
-#ifdef USV_DIAG_NOLIDAR
-    sc.rd0 = sc.rd1 = R(kSensorMax) + lox[k * cap]; sc.term = false; sc.far = false;
-#else
-    lidar_wave<R, LID>(RowSoA<R>{lox + k * cap, loy + k * cap, lor + k * cap}, n, sh.px[k], sh.py[k],
-                       sh.sp[k], sh.cp[k], rayoff, wslot, wmark, sc);
-#endif
-    const bool done = sc.term || sh.trunc[k];
-    const bool coll = ballot((sc.rd0 < R(kCollDist)) | (sc.rd1 < R(kCollDist))) != 0;  // :153-156
-    if (l == 0) { sh.term[k] = sc.term; sh.coll[k] = coll; }
-    const float s0 = (float)l_norm(sc.rd0), s1 = (float)l_norm(sc.rd1);          // :82-83
-    const bool reset_now = done && S.autoreset == USV_AUTORESET_SAME_STEP;
-    float* row = io.obs + (size_t)e * kObsDim;
-    row[kHdr + l] = s0;                                        // stale scan is kept by reset
-    row[kHdr + 64 + l] = s1;
-    if (done && io.fobs) {                                     // terminal obs (header from phase 1)
-      float* f = io.fobs + (size_t)e * kObsDim;
-      f[kHdr + l] = s0;
-      f[kHdr + 64 + l] = s1;
-      if (l < kHdr) f[l] = row[l];
-    }
-    if (reset_now) {
-      S.sensor_last[(size_t)e * kSensors + l] = sc.rd0;
-      S.sensor_last[(size_t)e * kSensors + 64 + l] = sc.rd1;
-    }
-  }
-  if (wave == 0) USV_STAMP(3);
-  // same-step autoreset of this wave's done envs (own loop: keeps the lidar loop's registers free)
-  if (S.autoreset == USV_AUTORESET_SAME_STEP) {
-    for (int k = wave; k < ne; k += kWaves)
-      if (sh.term[k] | sh.trunc[k]) reset_wave<R, MODE>(S, e0 + k, io.obs + (size_t)(e0 + k) * kObsDim);
-  }
-  if (wave == 0) USV_STAMP(4);
-  __syncthreads();
-  USV_STAMP(5);
-
-  // ---- phase 3: lane-per-env reward and flags (coalesced)
-  if (tid < ne) {
-    const int e = e0 + tid;
-    const R coll = sh.coll[tid] ? R(-20) : R(0);                    // simple_env.py:153-156
-    io.rew[e] = coll + sh.partial[tid];
-    const bool term = sh.term[tid], trunc = sh.trunc[tid];
-    io.term[e] = term;
-    io.trunc[e] = trunc;
-  }
-  USV_STAMP(6);
-}
-
 // --------------------------------------------------------------------------- wave-per-env scan
 // Shared by the two fast step kernels (step_kernel_wave: dynamics + scan in one launch;
 // dyn_kernel + scan_kernel: split).  Each wave owns EPW consecutive envs and, after one block
@@ -1045,11 +1046,14 @@ __device__ __forceinline__ void step_body(const State<R>& S, const IO<R>& io) {
 // current ones are scanned; on the f32 window path two envs share each iteration.
 //
 // LDS: [ray table 128 x Vec2, block-shared]
-//      [per wave: pair slots 256 x u64 | owner marks 64 x i32 | row buffers 2 x (2 rows)]
+//      [per wave: pair slots 256 x u64 | owner marks 64 x i32 | row buffers 2 x (2 rows, >= 1 KiB)]
 __host__ __device__ constexpr size_t align16(size_t b) { return (b + 15) & ~(size_t)15; }
+__host__ __device__ constexpr int obst_stride(int cap) { return (cap + 3) & ~3; }
+template <typename R> __host__ __device__ constexpr int row_bytes(int cap) { return 3 * obst_stride(cap) * (int)sizeof(R); }
 template <typename R> __host__ __device__ constexpr size_t wave_tab_bytes() { return kSensors * 2 * sizeof(R); }
+// two rows, and at least the 64 x 16-B per-obstacle records lidar_window2 leaves in the buffer
 template <typename R> __host__ __device__ constexpr size_t scan_rowbuf_bytes(int cap) {
-  return align16(2 * (size_t)cap * sizeof(R4<R>));
+  return align16(std::max((size_t)2 * row_bytes<R>(cap), (size_t)1024));
 }
 template <typename R> __host__ __device__ constexpr size_t lds_scan_slice(int cap) {
   return 256 * 8 + 64 * 4 + 2 * scan_rowbuf_bytes<R>(cap);
@@ -1089,16 +1093,16 @@ template <typename R> struct ScanLds {
   typename Vec2<R>::T* rayoff;
   unsigned long long* slot;
   int* mark;
-  R4<R>* row0;
-  R4<R>* row1;
+  R* row0;
+  R* row1;
 };
 template <typename R>
 __device__ __forceinline__ ScanLds<R> scan_lds(char* lds, int wave, int cap) {
   char* w = lds + wave_tab_bytes<R>() + wave * lds_scan_slice<R>(cap);
-  R4<R>* r0 = reinterpret_cast<R4<R>*>(w + 256 * 8 + 64 * 4);
+  R* r0 = reinterpret_cast<R*>(w + 256 * 8 + 64 * 4);
   return ScanLds<R>{reinterpret_cast<typename Vec2<R>::T*>(lds), reinterpret_cast<unsigned long long*>(w),
                     reinterpret_cast<int*>(w + 256 * 8), r0,
-                    reinterpret_cast<R4<R>*>(reinterpret_cast<char*>(r0) + scan_rowbuf_bytes<R>(cap))};
+                    reinterpret_cast<R*>(reinterpret_cast<char*>(r0) + scan_rowbuf_bytes<R>(cap))};
 }
 // envs per scan iteration: two on the f32 window path (<= 32 obstacle lanes per env)
 template <typename R, int LID> __device__ __forceinline__ int scan_step(int cap) {
@@ -1109,7 +1113,7 @@ template <typename R, int LID>
 __device__ __forceinline__ void scan_prologue(const State<R>& S, const ScanLds<R>& L, int wave, int e0, int ne) {
   const int cap = S.cap;
   if (wave == 0) dma_copy(S.ray_tab, L.rayoff, (int)wave_tab_bytes<R>());
-  if (ne > 0) dma_copy(S.obst + (size_t)e0 * cap, L.row0, min(scan_step<R, LID>(cap), ne) * cap * (int)sizeof(R4<R>));
+  if (ne > 0) dma_copy(S.orow(e0), L.row0, min(scan_step<R, LID>(cap), ne) * row_bytes<R>(cap));
 #pragma unroll
   for (int i = 0; i < 4; ++i) L.slot[i * 64 + lane_id()] = ~0ull;
 }
@@ -1169,7 +1173,7 @@ __device__ __forceinline__ void scan_envs(const State<R>& S, const IO<R>& io, co
                                           int ne, const R4<R>& P, int nl, unsigned trunc_m,
                                           unsigned& term_m, unsigned& coll_m, Prof& prof) {
   const int cap = S.cap;
-  const int rowb = cap * (int)sizeof(R4<R>);
+  const int rowb = row_bytes<R>(cap);
   const int step = scan_step<R, LID>(cap);
   term_m = 0; coll_m = 0;
   auto emit = [&](int k, const Scan<R>& sc) {               // outputs of env e0 + k
@@ -1177,7 +1181,7 @@ __device__ __forceinline__ void scan_envs(const State<R>& S, const IO<R>& io, co
   };
   const int iters = (ne + step - 1) / step;
   for (int k = 0; k < ne; k += step) {
-    R4<R>* cur = ((k / step) & 1) ? L.row1 : L.row0;
+    R* cur = ((k / step) & 1) ? L.row1 : L.row0;
     if (S.prio == 1) set_prio(3 - (4 * (k / step)) / iters);
     else if (S.prio == 2) set_prio(k + step >= ne ? 3 : 0);   // a wave's last iteration first
     prof.mark(4);
@@ -1187,24 +1191,21 @@ __device__ __forceinline__ void scan_envs(const State<R>& S, const IO<R>& io, co
       if (step == 2) vm_wait<4>(); else vm_wait<2>();
     }
     if (k + step < ne)
-      dma_copy(S.obst + (size_t)(e0 + k + step) * cap, ((k / step) & 1) ? L.row0 : L.row1,
-               min(step, ne - k - step) * rowb);
+      dma_copy(S.orow(e0 + k + step), ((k / step) & 1) ? L.row0 : L.row1, min(step, ne - k - step) * rowb);
     prof.mark(1);
     prof.count(7);
     if constexpr (std::is_same<R, float>::value && (LID & kLidWindow) != 0) {
       if (step == 2) {
         const bool hasB = k + 1 < ne;
-        const int kb = hasB ? k + 1 : k;
-        const Pose2 PP{bcast(P.x, k), bcast(P.y, k), bcast(P.z, k), bcast(P.w, k),
-                       bcast(P.x, kb), bcast(P.y, kb), bcast(P.z, kb), bcast(P.w, kb)};
+        const bool hb = lane_id() >= 32;
+        const int kl = hb ? k + 1 : k;             // this lane's env (B half: k + 1 if it exists)
+        const int kc = hasB ? kl : k;
+        const float lpx = __shfl(P.x, kc, kWave), lpy = __shfl(P.y, kc, kWave);
+        const float lsp = __shfl(P.z, kc, kWave), lcp = __shfl(P.w, kc, kWave);
+        const int lnl = (hb && !hasB) ? 0 : __shfl(nl, kc, kWave);
         Scan<float> sa, sb;
-#ifdef USV_ABL_NOLIDAR   // diagnostic ablation only: readings from the row, no scan
-        sa.rd0 = sb.rd0 = reinterpret_cast<const float4*>(cur)[lane_id() & 31].x + PP.pxA;
-        sa.rd1 = sb.rd1 = PP.pyB; sa.term = sb.term = false; sa.far = sb.far = false;
-#else
-        lidar_wave2(reinterpret_cast<float4*>(cur), cap, __builtin_amdgcn_readlane(nl, k),
-                    hasB ? __builtin_amdgcn_readlane(nl, kb) : 0, PP, L.rayoff, L.slot, L.mark, sa, sb);
-#endif
+        lidar_wave2(cur, obst_stride(cap), lnl, lpx, lpy, ray_c(lcp, lsp, (float)kStartC, (float)kStartS),
+                    ray_s(lcp, lsp, (float)kStartC, (float)kStartS), L.rayoff, L.slot, L.mark, sa, sb);
         prof.mark(2);
         emit(k, sa);
         if (hasB) emit(k + 1, sb);
@@ -1213,8 +1214,9 @@ __device__ __forceinline__ void scan_envs(const State<R>& S, const IO<R>& io, co
       }
     }
     Scan<R> sc;
-    lidar_wave<R, LID>(RowAoS<R>{cur}, __builtin_amdgcn_readlane(nl, k), bcast(P.x, k), bcast(P.y, k),
-                       bcast(P.z, k), bcast(P.w, k), L.rayoff, L.slot, L.mark, sc);
+    const int os = obst_stride(cap);
+    lidar_wave<R, LID>(RowSoA<R>{cur, cur + os, cur + 2 * os}, __builtin_amdgcn_readlane(nl, k), bcast(P.x, k),
+                       bcast(P.y, k), bcast(P.z, k), bcast(P.w, k), L.rayoff, L.slot, L.mark, sc);
     prof.mark(2);
     emit(k, sc);
     prof.mark(3);
@@ -1271,7 +1273,8 @@ __device__ __forceinline__ void step_body_wave(const State<R>& S, const IO<R>& i
     px = S.F(F_X)[e]; py = S.F(F_Y)[e]; sp = R(a.x); cp = R(a.y); partial = R(0); trunc = false;
     for (int i = 0; i < kHdr; ++i) hdr[i] = (float)px;
 #else
-    env_dynamics<R, MODE>(S, e, a.x, a.y, hdr, px, py, sp, cp, partial, trunc);
+    env_dynamics<R, MODE>(S, e, a.x, a.y, hdr, px, py, sp, cp, partial, trunc,
+                             io.info ? io.info + (size_t)e * USV_INFO_DIM : nullptr);
 #endif
     float* row = io.obs + (size_t)e * kObsDim;
 #pragma unroll
@@ -1315,7 +1318,8 @@ __global__ __launch_bounds__(kBlock) void dyn_kernel(State<R> S, IO<R> io) {
   float hdr[kHdr];
   R px, py, sp, cp, partial;
   bool trunc;
-  env_dynamics<R, MODE>(S, e, a.x, a.y, hdr, px, py, sp, cp, partial, trunc);
+  env_dynamics<R, MODE>(S, e, a.x, a.y, hdr, px, py, sp, cp, partial, trunc,
+                             io.info ? io.info + (size_t)e * USV_INFO_DIM : nullptr);
   float* row = io.obs + (size_t)e * kObsDim;
 #pragma unroll
   for (int i = 0; i < kHdr; ++i) row[i] = hdr[i];
@@ -1369,76 +1373,122 @@ __global__ __launch_bounds__(kWave * WPB) void scan_kernel(State<R> S, IO<R> io)
 }
 
 // ---- block-queue step (f32 window lidar, cap <= 32): 1024-thread blocks of 16 waves own
-// kQEnvs envs each; the block's env pairs are pulled from an LDS counter.  VALU issue on a SIMD
-// is arbitrated by priority, then age, so with a static split the oldest waves finish first
-// and the youngest run alone at the end; with the queue the favoured waves simply take more
-// pairs and all of them finish together.  The block's queue position also sets every wave's
-// priority (lagging blocks first), which evens out the two blocks that share each SIMD.
-//   kind 5 (fused): waves 0 and 1 run the block's dynamics lane-per-env (full width) and leave
-//                   the pose records in LDS;
-//   kind 4 (split): dyn_kernel ran first and left them in S.pose; they are DMA'd into LDS.
+// kQE = 128 envs each; the block's env pairs are pulled from an LDS counter.  VALU issue on a
+// SIMD is arbitrated by priority, then age, so with a static split the oldest waves finish first
+// and the youngest run alone at the end; with the queue the favoured waves simply take more pairs
+// and all of them finish together.
+//   fused (usv-simple): waves 0 and 1 run the block's dynamics lane-per-env (full width) and
+//                       leave one 64-B record per env in LDS;
+//   split (usv-asmc-simple): dyn_rec_kernel ran first and left the records in S.qrec; they are
+//                       DMA'd into LDS.
+// Record (16 f32): pose (x, y, ray-0 direction c0, s0) | partial reward, n_obs | truncated << 16
+// (int bits), then the non-constant obs-header values h0, h2..h9, h11 (make_header).  The obs
+// header is stored together with the sensors when the env's pair is scanned, so each obs row is
+// written once, late, and as a whole (no early header stores to lines that would be evicted
+// before the sensors reach them).
 // Each wave's first pair is static (pair = wave); its rows and the next pair's are DMA'd while
-// the current pair is scanned.
-// QW waves per block, QE envs per block (QE / 64 waves run the dynamics): (8, 64), (16, 128), or
-// (16, 256) padded past 80 KiB of LDS so that exactly one block fits a CU -- then one queue
-// balances the whole CU and no block is starved by an older one on the same SIMDs.
-__host__ __device__ constexpr size_t lds_q_bytes(int cap, int qw, int qe) {
-  return std::max(wave_tab_bytes<float>() + qw * lds_scan_slice<float>(cap) + qe * 2 * 16 + 16,
-                  qe > 8 * qw ? (size_t)82 * 1024 : (size_t)0);
+// the current pair is scanned (one DMA instruction per pair: two 384-B SoA rows).
+constexpr int kQW = 16, kQE = 128, kQRec = 16;
+__host__ __device__ constexpr size_t q_slice_bytes() { return 256 * 8 + 64 * 4 + 2 * 1024; }
+__host__ __device__ constexpr size_t lds_q_bytes() {
+  return wave_tab_bytes<float>() + kQW * q_slice_bytes() + kQE * kQRec * 4 + 16;
+}
+static_assert(2 * lds_q_bytes() <= 160 * 1024, "two blocks per CU");
+
+// One DMA instruction (<= 64 pieces of 16 B, i.e. <= 1 KiB): pieces c >= nchunk are not copied.
+__device__ __forceinline__ void dma_copy1(const void* src, void* dst, int bytes) {
+  const int c = lane_id();
+  const unsigned d = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)dst);
+  if (c < bytes / 16) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(reinterpret_cast<const char*>(src) + 16 * (size_t)c), "s"(d) : "memory");
+  }
 }
 
-template <int MODE, bool FUSED, int QW, int QE>
+__device__ __forceinline__ void make_qrec(float* rec, float px, float py, float sp, float cp, float partial,
+                                          int n, bool trunc, const float (&h)[kHdr]) {
+  const float c0 = ray_c(cp, sp, (float)kStartC, (float)kStartS), s0 = ray_s(cp, sp, (float)kStartC, (float)kStartS);
+  float4* r4 = reinterpret_cast<float4*>(rec);
+  r4[0] = make_float4(px, py, c0, s0);
+  r4[1] = make_float4(partial, __int_as_float(n | (trunc ? 1 << 16 : 0)), h[0], h[2]);
+  r4[2] = make_float4(h[3], h[4], h[5], h[6]);
+  r4[3] = make_float4(h[7], h[8], h[9], h[11]);
+}
+// obs-header value i (0..14) of the env whose record is `rec` (make_header's layout: entries 1, 10,
+// 13 are 0, entries 12, 14 the max_acceleration constants)
+__device__ __forceinline__ float qrec_hdr(const float* rec, int i) {
+  const float v = rec[i == 0 ? 6 : (i <= 9 ? i + 5 : 15)];
+  return (i == 1 || i == 10 || i == 13) ? 0.0f
+       : i == 12 ? (float)(kMaxAccU / 10.0) : i == 14 ? (float)(kMaxAccR / 10.0) : v;
+}
+
+// Terminal obs and stale scan of a done env e (rare path; lane l holds its rays l, l + 64).
+__device__ __forceinline__ void q_emit_done(const State<float>& S, const IO<float>& io, int e,
+                                            const Scan<float>& sc, const float* rec) {
+  const int l = lane_id();
+  if (io.fobs) {
+    float* f = io.fobs + (size_t)e * kObsDim;
+    f[kHdr + l] = l_norm(sc.rd0);
+    f[kHdr + 64 + l] = l_norm(sc.rd1);
+    const int hi = min(l, kHdr - 1);
+    f[hi] = qrec_hdr(rec, hi);
+  }
+  if (S.autoreset == USV_AUTORESET_SAME_STEP) {
+    S.sensor_last[(size_t)e * kSensors + l] = sc.rd0;
+    S.sensor_last[(size_t)e * kSensors + 64 + l] = sc.rd1;
+  }
+}
+
+template <int MODE, bool FUSED>
 __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<float>& io) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  constexpr int kQWaves = QW, kQEnvs = QE;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const int l = lane_id();
-  const int cap = S.cap, rowb = cap * (int)sizeof(float4);
-  const int eb = blockIdx.x * kQEnvs;                  // this block's envs: eb .. eb + nbe - 1
-  const int nbe = min(kQEnvs, S.N - eb);
+  const int os = S.ostride, rowb = row_bytes<float>(S.cap);
+  const int eb = blockIdx.x * kQE;                     // this block's envs: eb .. eb + nbe - 1
+  const int nbe = min(kQE, S.N - eb);
   const int np = (nbe + 1) >> 1;                       // and pairs 0 .. np - 1 (block-local)
-  const ScanLds<float> L = scan_lds<float>(lds, wave, cap);
-  R4<float>* const rec = reinterpret_cast<R4<float>*>(lds + wave_tab_bytes<float>() + kQWaves * lds_scan_slice<float>(cap));
-  unsigned* const qctr = reinterpret_cast<unsigned*>(rec + 2 * kQEnvs);
-  if (threadIdx.x == 0) *qctr = kQWaves;                // pairs 0 .. kQWaves-1 are the static first ones
-  if (wave == 0) dma_copy(S.ray_tab, L.rayoff, (int)wave_tab_bytes<float>());
+  char* const slice = lds + wave_tab_bytes<float>() + wave * q_slice_bytes();
+  unsigned long long* const slot = reinterpret_cast<unsigned long long*>(slice);
+  int* const mark = reinterpret_cast<int*>(slice + 256 * 8);
+  float* const rowbuf0 = reinterpret_cast<float*>(slice + 256 * 8 + 64 * 4);
+  float* const rowbuf1 = rowbuf0 + 256;
+  float* const recs = reinterpret_cast<float*>(lds + wave_tab_bytes<float>() + kQW * q_slice_bytes());
+  unsigned* const qctr = reinterpret_cast<unsigned*>(recs + kQE * kQRec);
+  const float2* const rayoff = reinterpret_cast<const float2*>(lds);
+  if (threadIdx.x == 0) *qctr = kQW;                   // pairs 0 .. kQW-1 are the static first ones
+  if (wave == 0) dma_copy(S.ray_tab, lds, (int)wave_tab_bytes<float>());
 #pragma unroll
-  for (int i = 0; i < 4; ++i) L.slot[i * 64 + l] = ~0ull;
+  for (int i = 0; i < 4; ++i) slot[i * 64 + l] = ~0ull;
   USV_STAMP_W(0);
   USV_STAMP_ID();
   int cur = wave;
-  if (cur < np) dma_copy(S.obst + (size_t)(eb + 2 * cur) * cap, L.row0, min(2, nbe - 2 * cur) * rowb);
+  if (cur < np) dma_copy1(S.orow(eb + 2 * cur), rowbuf0, min(2, nbe - 2 * cur) * rowb);
   if constexpr (FUSED) {
-    // phase 1: dynamics, one lane per env.  Lanes past the end repeat the wave's last env (same
-    // wave: every lane loads the state before any lane stores it); a wave with no env of its
-    // own must not run, or two waves would race on the same env's state
-    if (wave < kQEnvs / kWave && wave * kWave < nbe) {
+    // dynamics, one lane per env.  Lanes past the end repeat the wave's last env (same wave:
+    // every lane loads the state before any lane stores it); a wave with no env of its own must
+    // not run, or two waves would race on the same env's state
+    if (wave < kQE / kWave && wave * kWave < nbe) {
       const int k = min(wave * kWave + l, nbe - 1);
       const int e = eb + k;
       const float2 a = reinterpret_cast<const float2*>(io.act)[e];
       float hdr[kHdr];
       float px, py, sp, cp, partial;
       bool trunc;
-      env_dynamics<float, MODE>(S, e, a.x, a.y, hdr, px, py, sp, cp, partial, trunc);
-      float* row = io.obs + (size_t)e * kObsDim;
-#pragma unroll
-      for (int i = 0; i < kHdr; ++i) row[i] = hdr[i];
+      env_dynamics<float, MODE>(S, e, a.x, a.y, hdr, px, py, sp, cp, partial, trunc,
+                                io.info ? io.info + (size_t)e * USV_INFO_DIM : nullptr);
       io.trunc[e] = trunc;
-      rec[2 * k] = R4<float>{px, py, sp, cp};
-      rec[2 * k + 1] = R4<float>{partial, (float)S.I(I_NOBS)[e], trunc ? 1.0f : 0.0f, 0.0f};
+      make_qrec(recs + k * kQRec, px, py, sp, cp, partial, S.I(I_NOBS)[e], trunc, hdr);
     }
   } else {
-    if (wave < kQEnvs / kWave && wave * kWave < nbe)    // 64 records (2 KiB) per wave
-      dma_copy(S.pose + 2 * (size_t)(eb + wave * kWave), rec + 2 * wave * kWave, min(kWave, nbe - wave * kWave) * 32);
+    if (wave < kQE / 16 && wave * 16 < nbe)            // 16 records (1 KiB) per wave
+      dma_copy1(S.qrec + (size_t)(eb + wave * 16) * kQRec, recs + wave * 16 * kQRec, min(16, nbe - wave * 16) * kQRec * 4);
   }
-  // rows, ray table and records landed; the dynamics' header stores are complete before the
-  // barrier, so a done env's terminal obs can copy its header from the obs row
+  // rows, ray table and records landed
   USV_STAMP_W(1);
-#ifdef USV_DIAG_NOSTOREWAIT   // diagnostic timing only: header stores may still be in flight
-  vm_wait<8>();
-#else
   vm_wait<0>();
-#endif
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   USV_STAMP_W(2);
   unsigned tk = 0;
@@ -1446,52 +1496,65 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
   // same-step autoresets of a pair run outside the pair loop (the loop is left after a pair with
   // a done env and re-entered): inside it their registers would spill the loop's to scratch
   int it = 0;
+  const bool hb = l >= 32;
   for (;;) {
     unsigned done = 0;
     int de0 = 0;
     for (; cur < np; ++it) {
-      R4<float>* cbuf = (it & 1) ? L.row1 : L.row0;
-      R4<float>* nbuf = (it & 1) ? L.row0 : L.row1;
-      const int e0 = eb + 2 * cur;
-      const bool hasB = 2 * cur + 1 < nbe;
-      const int kb = hasB ? 2 * cur + 1 : 2 * cur;
-      // records: wave-uniform LDS reads, moved to SGPRs
-      auto uni = [](float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); };
-      const R4<float> pa = rec[4 * cur], ma = rec[4 * cur + 1], pb = rec[2 * kb], mb = rec[2 * kb + 1];
-      const Pose2 PP{uni(pa.x), uni(pa.y), uni(pa.z), uni(pa.w), uni(pb.x), uni(pb.y), uni(pb.z), uni(pb.w)};
-      const int nA = (int)uni(ma.y), nB = hasB ? (int)uni(mb.y) : 0;
-      const unsigned trunc_m = (uni(ma.z) != 0.0f ? 1u : 0u) | (hasB && uni(mb.z) != 0.0f ? 2u : 0u);
-      const float part = (hasB && l >= 1) ? mb.x : ma.x;    // lane-per-env: lanes >= nb repeat
+      float* const cbuf = (it & 1) ? rowbuf1 : rowbuf0;
+      float* const nbuf = (it & 1) ? rowbuf0 : rowbuf1;
+      const int k0 = 2 * cur;
+      const int e0 = eb + k0;
+      const bool hasB = k0 + 1 < nbe;
       const int nxt = (int)__builtin_amdgcn_readlane(tk, 0);
-      if (S.prio == 1) set_prio(3 - (4 * min(nxt, np)) / (np + 1));
-      else if (S.prio == 2) set_prio(nxt >= np ? 3 : 0);     // the block's last pairs first
       if (nxt < np) {                                   // wave-uniform
         if (l == 0) tk = atomicAdd(qctr, 1u);
-        dma_copy(S.obst + (size_t)(eb + 2 * nxt) * cap, nbuf, min(2, nbe - 2 * nxt) * rowb);
+        dma_copy1(S.orow(eb + 2 * nxt), nbuf, min(2, nbe - 2 * nxt) * rowb);
       }
+      // this lane's env: lanes 0..31 env A, 32..63 env B (env A again when there is no B)
+      const int kl = (hb && hasB) ? k0 + 1 : k0;
+      const float* const rk = recs + kl * kQRec;
+      const float4 pose = *reinterpret_cast<const float4*>(rk);
+      const float4 meta = *reinterpret_cast<const float4*>(rk + 4);
+      const int nt = __float_as_int(meta.y);
       Scan<float> sa, sb;
-#ifdef USV_ABL_NOLIDAR   // diagnostic ablation only: readings from the row, no scan
-      sa.rd0 = sb.rd0 = reinterpret_cast<const float4*>(cbuf)[l & 31].x + PP.pxA;
-      sa.rd1 = sb.rd1 = PP.pyB; sa.term = sb.term = false; sa.far = sb.far = false;
-#else
-      lidar_wave2(reinterpret_cast<float4*>(cbuf), cap, nA, nB, PP, L.rayoff, L.slot, L.mark, sa, sb);
-#endif
-      unsigned term_m = 0, coll_m = 0;
-      const int nb = hasB ? 2 : 1;
-      for (int k = 0; k < nb; ++k)
-        emit_env<float, MODE>(S, io, e0 + k, k ? sb : sa, (trunc_m >> k) & 1, k, term_m, coll_m);
-      {                                                 // lanes 0, 1 (lanes >= nb repeat)
-        const int k = min(l, nb - 1);
-        const bool coll = (coll_m >> k) & 1;            // simple_env.py:153-156
-        io.rew[e0 + k] = coll ? -20.0f + part : part;
-        io.term[e0 + k] = (term_m >> k) & 1;
+      lidar_wave2(cbuf, os, (hb && !hasB) ? 0 : (nt & 0xffff), pose.x, pose.y, pose.z, pose.w, rayoff, slot,
+                  mark, sa, sb);
+      // env B's outputs (env A's again when there is none: identical stores to the same addresses
+      // keep every memory instruction of the loop non-divergent and its count static)
+      const int eB = hasB ? e0 + 1 : e0;
+      const float sB0 = hasB ? sb.rd0 : sa.rd0, sB1 = hasB ? sb.rd1 : sa.rd1;
+      const bool collA = ballot((sa.rd0 < (float)kCollDist) | (sa.rd1 < (float)kCollDist)) != 0;   // :153-156
+      const bool collB = hasB ? ballot((sb.rd0 < (float)kCollDist) | (sb.rd1 < (float)kCollDist)) != 0 : collA;
+      const bool termB = hasB ? sb.term : sa.term;
+      float* const rowA = io.obs + (size_t)e0 * kObsDim;
+      float* const rowB = io.obs + (size_t)eB * kObsDim;
+      rowA[kHdr + l] = l_norm(sa.rd0);                  // sensors (:82-83)
+      rowA[kHdr + 64 + l] = l_norm(sa.rd1);
+      rowB[kHdr + l] = l_norm(sB0);
+      rowB[kHdr + 64 + l] = l_norm(sB1);
+      {                                                 // headers: lanes 0..14 env A, 15..29 env B
+        const int hl = min(l, 2 * kHdr - 1);
+        const bool hB = hl >= kHdr && hasB;
+        const int hi = hl >= kHdr ? hl - kHdr : hl;
+        (hB ? rowB : rowA)[hi] = qrec_hdr(recs + (hB ? k0 + 1 : k0) * kQRec, hi);
       }
-      // the next pair's rows landed: at least four stores (two sensor-row stores per env, the
-      // reward and the terminated flag) were issued after their DMA
-      vm_wait<4>();
+      const bool term_l = hb ? termB : sa.term;         // reward, terminated: lanes 0..31 env A,
+      const bool coll_l = hb ? collB : collA;           // 32..63 env B
+      io.rew[eb + kl] = coll_l ? -20.0f + meta.x : meta.x;
+      io.term[eb + kl] = term_l;
+      const unsigned long long dm = ballot(term_l | ((nt >> 16) & 1));
+      const bool doneA = (unsigned)dm != 0, doneB = hasB && (dm >> 32) != 0;
+      if (doneA | doneB) {
+        if (doneA) q_emit_done(S, io, e0, sa, recs + k0 * kQRec);
+        if (doneB) q_emit_done(S, io, e0 + 1, sb, recs + (k0 + 1) * kQRec);
+      }
+      // the next pair's rows landed: at least seven stores (four sensor halves, the headers, the
+      // rewards and the terminated flags) were issued after their DMA
+      vm_wait<7>();
       cur = nxt;
-      if (S.autoreset == USV_AUTORESET_SAME_STEP && (term_m | trunc_m)) {
-        done = term_m | trunc_m;
+      if (S.autoreset == USV_AUTORESET_SAME_STEP && (doneA | doneB)) {
+        done = (doneA ? 1u : 0u) | (doneB ? 2u : 0u);
         de0 = e0;
         ++it;
         break;
@@ -1504,24 +1567,26 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
     }
   }
   USV_STAMP_W(3);
-  USV_STAMP_W(6);
 }
 
-template <int MODE, bool FUSED, int QW, int QE>
-__global__ __launch_bounds__(QW * kWave) __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8)))
-void step_q_kernel(State<float> S, IO<float> io) { step_q_body<MODE, FUSED, QW, QE>(S, io); }
+template <int MODE, bool FUSED>
+__global__ __launch_bounds__(kQW * kWave) __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8)))
+void step_q_kernel(State<float> S, IO<float> io) { step_q_body<MODE, FUSED>(S, io); }
 
-// 8 blocks of 256 threads per CU need <= 64 VGPRs and .sgpr_count <= 80 (MI355X_MICROARCH.md,
-// residency: 800 / (ceil(sgpr/16)*16 + 16) blocks; the occupancy API over-reports in 81..96).
-// The f32 usv-simple body fits; the ASMC and f64 bodies need more registers and run at the
-// occupancy their register use allows.
-template <typename R, int MODE, int EPB, int LID>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(80), amdgpu_num_vgpr(64)))
-void step_kernel_tight(State<R> S, IO<R> io) { step_body<R, MODE, EPB, LID>(S, io); }
-
-template <typename R, int MODE, int EPB, int LID>
-__global__ __launch_bounds__(kBlock) void step_kernel(State<R> S, IO<R> io) {
-  step_body<R, MODE, EPB, LID>(S, io);
+// Split block-queue step, first half: full-width lane-per-env dynamics writing the env records
+// (make_qrec) for step_q_kernel<MODE, false>, plus truncated and the info row.
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void dyn_rec_kernel(State<float> S, IO<float> io) {
+  const int e = blockIdx.x * kBlock + threadIdx.x;
+  if (e >= S.N) return;
+  const float2 a = reinterpret_cast<const float2*>(io.act)[e];
+  float hdr[kHdr];
+  float px, py, sp, cp, partial;
+  bool trunc;
+  env_dynamics<float, MODE>(S, e, a.x, a.y, hdr, px, py, sp, cp, partial, trunc,
+                            io.info ? io.info + (size_t)e * USV_INFO_DIM : nullptr);
+  io.trunc[e] = trunc;
+  make_qrec(S.qrec + (size_t)e * kQRec, px, py, sp, cp, partial, S.I(I_NOBS)[e], trunc, hdr);
 }
 
 // --------------------------------------------------------------------------- reset kernel
@@ -1555,8 +1620,8 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(State<R> S, IO<R> io) {
       heading_sincos(S.F(F_PSI)[e], &sp, &cp);
       const int n = uniform(S.I(I_NOBS)[e]);
       if (l < S.cap) {
-        const R4<R> o = S.obst[(size_t)e * S.cap + l];
-        wx[l] = o.x; wy[l] = o.y; wr[l] = o.z;
+        const R* o = S.orow(e);
+        wx[l] = o[l]; wy[l] = o[S.ostride + l]; wr[l] = o[2 * S.ostride + l];
       }
       Scan<R> sc;
       lidar_wave<R, kLidDefault>(RowSoA<R>{wx, wy, wr}, n, S.F(F_X)[e], S.F(F_Y)[e], sp, cp, rayoff,
@@ -1572,10 +1637,16 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(State<R> S, IO<R> io) {
     float* row = io.obs + (size_t)e * kObsDim;
     row[kHdr + l] = (float)l_norm(rd0);
     row[kHdr + 64 + l] = (float)l_norm(rd1);
+    float* info = io.info ? io.info + (size_t)e * USV_INFO_DIM : nullptr;
     if (S.np_reset) {
-      if (l == 0) np_reset<R, MODE>(S, e, row);
+      if (l == 0) np_reset<R, MODE>(S, e, row, info, io.kpath);
     } else {
-      reset_wave<R, MODE>(S, e, row);
+      const int ep = uniform(S.I(I_EPISODE)[e]);
+      reset_wave<R, MODE>(S, e, row, info, io.kpath);
+      if (S.exp) {
+        __threadfence_block();                 // the wave's reset stores land before lane 0 rewrites
+        if (l == 0) reset_experiment<R>(S, e, ep, row, info);
+      }
     }
   }
 }
@@ -1981,6 +2052,7 @@ struct Handle {
   int epb = 64, lid = 7, kind = 1;
   int prio = 1;                        // scan loops raise the priority of lagging waves
   void* slab = nullptr;
+  void* exp_buf = nullptr;             // device usv_experiment record (kExp* layout, in R)
   State<float> sf{};
   State<double> sd{};
 };
@@ -2003,9 +2075,10 @@ int carve(Handle* h, State<R>& S) {
   auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
   const size_t stride = al(N * sizeof(R)) / sizeof(R);   // also >= N int32 (sizeof(R) >= 4)
   const size_t bytes = F_NREAL * stride * sizeof(R) + al(I_NINT * stride * 4) +
-                       al(N * cap * sizeof(R4<R>)) + al(N * kSensors * sizeof(R)) +
+                       al(N * 3 * obst_stride((int)cap) * sizeof(R)) + al(N * kSensors * sizeof(R)) +
                        al((size_t)kAsmcN * N * sizeof(R)) + al((size_t)kV0N * stride * sizeof(R)) +
                        al(2 * kSensors * sizeof(R)) + al(2 * N * sizeof(R4<R>)) + al(10 * stride * 4) +
+                       al((kExpObs + 3 * cap) * sizeof(R)) + al(N * kQRec * sizeof(float)) +
                        (is_legacy(h->cfg.mode) ? al(625 * stride * 4) : 0);
   HIP_TRY(hipMalloc(&h->slab, bytes));
   HIP_TRY(hipMemset(h->slab, 0, bytes));
@@ -2014,14 +2087,19 @@ int carve(Handle* h, State<R>& S) {
   S.freal = (R*)take(F_NREAL * stride * sizeof(R));
   S.fint = (int32_t*)take(I_NINT * stride * 4);
   S.fstride = (int)stride;
-  S.obst = (R4<R>*)take(N * cap * sizeof(R4<R>));
+  S.ostride = obst_stride((int)cap);
+  S.obst = (R*)take(N * 3 * S.ostride * sizeof(R));
   S.sensor_last = (R*)take(N * kSensors * sizeof(R));
   S.asmc = (R*)take((size_t)kAsmcN * N * sizeof(R));
   S.v0 = (R*)take((size_t)kV0N * stride * sizeof(R));
   R* tab = (R*)take(2 * kSensors * sizeof(R));
   S.ray_tab = tab;
   S.pose = (R4<R>*)take(2 * N * sizeof(R4<R>));
+  S.qrec = (float*)take(N * kQRec * sizeof(float));
   S.nprng = (uint32_t*)take(10 * stride * 4);
+  h->exp_buf = take((kExpObs + 3 * cap) * sizeof(R));
+  S.exp = nullptr;                                       // usv_set_experiment installs it
+  S.perturb = (h->cfg.flags & USV_FLAG_PERTURB) != 0;
   S.npmt = is_legacy(h->cfg.mode) ? (uint32_t*)take(625 * stride * 4) : nullptr;   // legacy ids only
   S.np_reset = 0;
   S.N = h->cfg.num_envs;
@@ -2049,34 +2127,6 @@ int carve(Handle* h, State<R>& S) {
 
 // Step-kernel variants: envs per block x lidar variant.  Selected per handle at create time
 // (USV_STEP_VARIANT="epb,lid" overrides, for tuning sweeps); all variants are bit-identical.
-
-template <typename R, int MODE, int EPB>
-void* pick_lid(int lid) {
-  if constexpr (std::is_same<R, float>::value && MODE == USV_MODE_SIMPLE) {
-    switch (lid) {
-      case 0: return (void*)&step_kernel_tight<R, MODE, EPB, 0>;
-      case 1: return (void*)&step_kernel_tight<R, MODE, EPB, 1>;
-      case 2: return (void*)&step_kernel_tight<R, MODE, EPB, 2>;
-      case 3: return (void*)&step_kernel_tight<R, MODE, EPB, 3>;
-      case 5: return (void*)&step_kernel_tight<R, MODE, EPB, 5>;
-      default: return (void*)&step_kernel_tight<R, MODE, EPB, 7>;
-    }
-  }
-  switch (lid) {
-    case 0: return (void*)&step_kernel<R, MODE, EPB, 0>;
-    case 1: return (void*)&step_kernel<R, MODE, EPB, 1>;
-    case 2: return (void*)&step_kernel<R, MODE, EPB, 2>;
-    case 3: return (void*)&step_kernel<R, MODE, EPB, 3>;
-    case 5: return (void*)&step_kernel<R, MODE, EPB, 5>;
-    default: return (void*)&step_kernel<R, MODE, EPB, 7>;
-  }
-}
-template <typename R, int MODE>
-void* pick_step(int epb, int lid) {
-  if (epb == 16) return pick_lid<R, MODE, 16>(lid);
-  if (epb == 32) return pick_lid<R, MODE, 32>(lid);
-  return pick_lid<R, MODE, 64>(lid);
-}
 
 template <typename R, int MODE, int EPW>
 void* pick_wave_lid(int lid) {
@@ -2110,38 +2160,35 @@ void* pick_scan_lid(int lid) {
 }
 template <typename R, int MODE, int WPB>
 void* pick_scan(int epw, int lid) {
-  if (epw == 1) return pick_scan_lid<R, MODE, 1, WPB>(lid);
   if (epw == 2) return pick_scan_lid<R, MODE, 2, WPB>(lid);
   if (epw == 8) return pick_scan_lid<R, MODE, 8, WPB>(lid);
   return pick_scan_lid<R, MODE, 4, WPB>(lid);
 }
 
-template <int QW, int QE>
-void* pick_q_mode(int mode, bool fused) {
+void* pick_q(int mode, bool fused) {
   const bool simple = mode == USV_MODE_SIMPLE;
-  if (fused) return simple ? (void*)&step_q_kernel<USV_MODE_SIMPLE, true, QW, QE> : (void*)&step_q_kernel<USV_MODE_ASMC_SIMPLE, true, QW, QE>;
-  return simple ? (void*)&step_q_kernel<USV_MODE_SIMPLE, false, QW, QE> : (void*)&step_q_kernel<USV_MODE_ASMC_SIMPLE, false, QW, QE>;
-}
-int q_waves(int qe) { return qe == 64 ? 8 : 16; }
-void* pick_q(int mode, bool fused, int qe) {
-  if (qe == 64) return pick_q_mode<8, 64>(mode, fused);
-  if (qe == 256) return pick_q_mode<16, 256>(mode, fused);
-  return pick_q_mode<16, 128>(mode, fused);
+  if (fused) return simple ? (void*)&step_q_kernel<USV_MODE_SIMPLE, true> : (void*)&step_q_kernel<USV_MODE_ASMC_SIMPLE, true>;
+  return simple ? (void*)&step_q_kernel<USV_MODE_SIMPLE, false> : (void*)&step_q_kernel<USV_MODE_ASMC_SIMPLE, false>;
 }
 
 template <typename R>
 int launch_step_kernels(Handle* h, State<R>& S, const float* act, float* obs, void* rew, uint8_t* term,
-                        uint8_t* trunc, float* fobs, hipStream_t st);
+                        uint8_t* trunc, float* fobs, float* info, hipStream_t st);
 
 // The step, then (NumPy-exact reset mode) the resets of the envs that ended in it.
 template <typename R>
 int launch_step(Handle* h, State<R>& S, const float* act, float* obs, void* rew, uint8_t* term,
-                uint8_t* trunc, float* fobs, hipStream_t st) {
-  const int rc = launch_step_kernels(h, S, act, obs, rew, term, trunc, fobs, st);
+                uint8_t* trunc, float* fobs, float* info, hipStream_t st) {
+  const int rc = launch_step_kernels(h, S, act, obs, rew, term, trunc, fobs, info, st);
   // (the legacy kernels reset inline, from the MT19937 state, in the NumPy-exact mode too)
-  if (rc != USV_OK || !S.np_reset || S.autoreset != USV_AUTORESET_SAME_STEP || is_legacy(h->cfg.mode)) return rc;
-  IO<R> io{act, obs, (R*)rew, term, trunc, fobs, nullptr};
+  if (rc != USV_OK || S.autoreset != USV_AUTORESET_SAME_STEP || is_legacy(h->cfg.mode)) return rc;
+  IO<R> io{act, obs, (R*)rew, term, trunc, fobs, nullptr, nullptr, 0};
   const dim3 grid((S.N + kBlock - 1) / kBlock), block(kBlock);
+  if (!S.np_reset) {
+    if (S.exp) hipLaunchKernelGGL((exp_autoreset_kernel<R>), grid, block, 0, st, S, io);
+    HIP_TRY(hipGetLastError());
+    return USV_OK;
+  }
   if (h->cfg.mode == USV_MODE_SIMPLE)
     hipLaunchKernelGGL((np_autoreset_kernel<R, USV_MODE_SIMPLE>), grid, block, 0, st, S, io);
   else
@@ -2152,8 +2199,8 @@ int launch_step(Handle* h, State<R>& S, const float* act, float* obs, void* rew,
 
 template <typename R>
 int launch_step_kernels(Handle* h, State<R>& S, const float* act, float* obs, void* rew, uint8_t* term,
-                        uint8_t* trunc, float* fobs, hipStream_t st) {
-  IO<R> io{act, obs, (R*)rew, term, trunc, fobs, nullptr};
+                        uint8_t* trunc, float* fobs, float* info, hipStream_t st) {
+  IO<R> io{act, obs, (R*)rew, term, trunc, fobs, nullptr, is_legacy(h->cfg.mode) ? nullptr : info, 0};
   if (is_legacy(h->cfg.mode)) {
     const dim3 grid((S.N + kBlock - 1) / kBlock), block(kBlock);
     if (h->cfg.mode == USV_MODE_ASMC_V0)
@@ -2166,56 +2213,38 @@ int launch_step_kernels(Handle* h, State<R>& S, const float* act, float* obs, vo
     return USV_OK;
   }
   const int epb = h->epb, lid = h->lid;
-  void* fn;
-  size_t lds;
+  const bool simple = h->cfg.mode == USV_MODE_SIMPLE;
+  void* args[] = {(void*)&S, (void*)&io};
   if constexpr (std::is_same<R, float>::value) {
-    if (h->kind == 4 || h->kind == 5) {                     // block-queue step, epb envs per block
-      void* args[] = {(void*)&S, (void*)&io};
-      const bool simple = h->cfg.mode == USV_MODE_SIMPLE;
-      const int qw = q_waves(h->epb);
+    if (h->kind == 4 || h->kind == 5) {                     // block-queue step, kQE envs per block
       if (h->kind == 4) {
-        void* dyn = simple ? (void*)&dyn_kernel<R, USV_MODE_SIMPLE> : (void*)&dyn_kernel<R, USV_MODE_ASMC_SIMPLE>;
+        void* dyn = simple ? (void*)&dyn_rec_kernel<USV_MODE_SIMPLE> : (void*)&dyn_rec_kernel<USV_MODE_ASMC_SIMPLE>;
         HIP_TRY(hipLaunchKernel(dyn, dim3((S.N + kBlock - 1) / kBlock), dim3(kBlock), args, 0, st));
       }
-      void* fn = pick_q(h->cfg.mode, h->kind == 5, h->epb);
-      HIP_TRY(hipLaunchKernel(fn, dim3((S.N + h->epb - 1) / h->epb), dim3(qw * kWave), args,
-                              lds_q_bytes(S.cap, qw, h->epb), st));
+      HIP_TRY(hipLaunchKernel(pick_q(h->cfg.mode, h->kind == 5), dim3((S.N + kQE - 1) / kQE), dim3(kQW * kWave),
+                              args, lds_q_bytes(), st));
       return USV_OK;
     }
   }
-  if (h->kind == 2 || h->kind == 3) {                       // split: dynamics, then scan
-    void* args[] = {(void*)&S, (void*)&io};
-    void* dyn = h->cfg.mode == USV_MODE_SIMPLE ? (void*)&dyn_kernel<R, USV_MODE_SIMPLE>
-                                               : (void*)&dyn_kernel<R, USV_MODE_ASMC_SIMPLE>;
+  if (h->kind == 2) {                                       // split: dynamics, then the wave scan
+    void* dyn = simple ? (void*)&dyn_kernel<R, USV_MODE_SIMPLE> : (void*)&dyn_kernel<R, USV_MODE_ASMC_SIMPLE>;
     HIP_TRY(hipLaunchKernel(dyn, dim3((S.N + kBlock - 1) / kBlock), dim3(kBlock), args, 0, st));
-    if (h->kind == 2) {                                     // 4-wave blocks, epb envs each
-      fn = h->cfg.mode == USV_MODE_SIMPLE ? pick_scan<R, USV_MODE_SIMPLE, kWaves>(epb / kWaves, lid)
-                                          : pick_scan<R, USV_MODE_ASMC_SIMPLE, kWaves>(epb / kWaves, lid);
-      HIP_TRY(hipLaunchKernel(fn, dim3((S.N + epb - 1) / epb), dim3(kBlock), args, lds_scan_bytes<R>(S.cap), st));
-    } else {                                                // 1-wave blocks, epb envs each
-      fn = h->cfg.mode == USV_MODE_SIMPLE ? pick_scan<R, USV_MODE_SIMPLE, 1>(epb, lid)
-                                          : pick_scan<R, USV_MODE_ASMC_SIMPLE, 1>(epb, lid);
-      HIP_TRY(hipLaunchKernel(fn, dim3((S.N + epb - 1) / epb), dim3(kWave), args, lds_scan_bytes<R>(S.cap, 1), st));
-    }
+    void* fn = simple ? pick_scan<R, USV_MODE_SIMPLE, kWaves>(epb / kWaves, lid)
+                      : pick_scan<R, USV_MODE_ASMC_SIMPLE, kWaves>(epb / kWaves, lid);
+    HIP_TRY(hipLaunchKernel(fn, dim3((S.N + epb - 1) / epb), dim3(kBlock), args, lds_scan_bytes<R>(S.cap), st));
     return USV_OK;
   }
-  if (h->kind == 1) {
-    fn = h->cfg.mode == USV_MODE_SIMPLE ? pick_wave<R, USV_MODE_SIMPLE>(epb / kWaves, lid, &lds, S.cap)
-                                        : pick_wave<R, USV_MODE_ASMC_SIMPLE>(epb / kWaves, lid, &lds, S.cap);
-  } else {
-    fn = h->cfg.mode == USV_MODE_SIMPLE ? pick_step<R, USV_MODE_SIMPLE>(epb, lid)
-                                        : pick_step<R, USV_MODE_ASMC_SIMPLE>(epb, lid);
-    lds = lds_bytes<R>(epb, S.cap);
-  }
-  const dim3 grid((S.N + epb - 1) / epb), block(kBlock);
-  void* args[] = {(void*)&S, (void*)&io};
-  HIP_TRY(hipLaunchKernel(fn, grid, block, args, lds, st));
+  size_t lds;                                               // kind 1: fused wave kernel
+  void* fn = simple ? pick_wave<R, USV_MODE_SIMPLE>(epb / kWaves, lid, &lds, S.cap)
+                    : pick_wave<R, USV_MODE_ASMC_SIMPLE>(epb / kWaves, lid, &lds, S.cap);
+  HIP_TRY(hipLaunchKernel(fn, dim3((S.N + epb - 1) / epb), dim3(kBlock), args, lds, st));
   return USV_OK;
 }
 
 template <typename R>
-int launch_reset(Handle* h, State<R>& S, const uint8_t* mask, float* obs, hipStream_t st) {
-  IO<R> io{nullptr, obs, nullptr, nullptr, nullptr, nullptr, mask};
+int launch_reset(Handle* h, State<R>& S, const uint8_t* mask, float* obs, int kpath, float* info,
+                 hipStream_t st) {
+  IO<R> io{nullptr, obs, nullptr, nullptr, nullptr, nullptr, mask, is_legacy(h->cfg.mode) ? nullptr : info, kpath};
   const dim3 grid((S.N + kEPBReset - 1) / kEPBReset), block(kBlock);
   const dim3 lgrid((S.N + kBlock - 1) / kBlock);
   if (h->cfg.mode == USV_MODE_ASMC_V0)
@@ -2253,9 +2282,19 @@ int v0_base(int f) {
 
 // host <-> device for one field; host side [N][per] float64 / int32
 template <typename R>
+int field_io_impl(Handle* h, State<R>& S, int f, void* host, bool to_host);
+// Writes complete before returning (hipMemcpy from pageable memory may return before the DMA
+// lands), so a kernel the caller launches next on any stream sees them.
+template <typename R>
 int field_io(Handle* h, State<R>& S, int f, void* host, bool to_host) {
-  const size_t N = (size_t)S.N;
   HIP_TRY(hipDeviceSynchronize());
+  const int rc = field_io_impl(h, S, f, host, to_host);
+  if (rc == USV_OK && !to_host) HIP_TRY(hipDeviceSynchronize());
+  return rc;
+}
+template <typename R>
+int field_io_impl(Handle* h, State<R>& S, int f, void* host, bool to_host) {
+  const size_t N = (size_t)S.N;
   if (f < F_NREAL) {
     std::vector<R> tmp(N);
     double* hd = (double*)host;
@@ -2279,20 +2318,19 @@ int field_io(Handle* h, State<R>& S, int f, void* host, bool to_host) {
     else HIP_TRY(hipMemcpy(d, host, N * 4, hipMemcpyHostToDevice));
     return USV_OK;
   }
-  if (f >= USV_FIELD_OBS_X && f <= USV_FIELD_OBS_R) {
-    const size_t cnt = N * (size_t)S.cap;
-    std::vector<R4<R>> tmp(cnt);
-    HIP_TRY(hipMemcpy(tmp.data(), S.obst, cnt * sizeof(R4<R>), hipMemcpyDeviceToHost));
+  if (f >= USV_FIELD_OBS_X && f <= USV_FIELD_OBS_R) {   // device [N][3][ostride], host [N][cap]
+    const size_t os = (size_t)S.ostride, cnt = N * 3 * os, cap = (size_t)S.cap;
+    std::vector<R> tmp(cnt);
+    HIP_TRY(hipMemcpy(tmp.data(), S.obst, cnt * sizeof(R), hipMemcpyDeviceToHost));
     double* hd = (double*)host;
-    for (size_t i = 0; i < cnt; ++i) {
-      const int ci = f - USV_FIELD_OBS_X;      // component x / y / r
-      if (to_host) hd[i] = (double)tmp[i][ci];
-      else {
-        tmp[i][ci] = (R)hd[i];
-        if (f == USV_FIELD_OBS_R) tmp[i][3] = tmp[i][2] * tmp[i][2];
+    const size_t plane = (size_t)(f - USV_FIELD_OBS_X);   // x / y / r
+    for (size_t e = 0; e < N; ++e)
+      for (size_t j = 0; j < cap; ++j) {
+        R& v = tmp[(e * 3 + plane) * os + j];
+        if (to_host) hd[e * cap + j] = (double)v;
+        else v = (R)hd[e * cap + j];
       }
-    }
-    if (!to_host) HIP_TRY(hipMemcpy(S.obst, tmp.data(), cnt * sizeof(R4<R>), hipMemcpyHostToDevice));
+    if (!to_host) HIP_TRY(hipMemcpy(S.obst, tmp.data(), cnt * sizeof(R), hipMemcpyHostToDevice));
     return USV_OK;
   }
   if (f == USV_FIELD_SENSOR_LAST) {
@@ -2361,6 +2399,30 @@ size_t field_bytes(const Handle* h, int f) {
   return (size_t)h->cfg.num_envs * field_per_env(h, f) * (kFields[f].is_int ? 4 : 8);
 }
 
+template <typename R>
+int set_experiment(Handle* h, State<R>& S, const usv_experiment* x) {
+  HIP_TRY(hipDeviceSynchronize());                       // in-flight resets may read the old one
+  if (!x) {
+    S.exp = nullptr;
+    return USV_OK;
+  }
+  const int cap = h->cfg.obstacle_cap;
+  std::vector<R> v((size_t)kExpObs + 3 * cap, R(0));
+  v[kExpN] = (R)x->n_obs;
+  v[kExpPS] = (R)x->path_start[0]; v[kExpPS + 1] = (R)x->path_start[1];
+  v[kExpAngle] = (R)x->angle;
+  for (int i = 0; i < 3; ++i) v[kExpPose + i] = (R)x->position[i];
+  for (int j = 0; j < x->n_obs; ++j) {
+    v[kExpObs + j] = (R)x->obstacle_x[j];
+    v[kExpObs + cap + j] = (R)x->obstacle_y[j];
+    v[kExpObs + 2 * cap + j] = (R)x->obstacle_r[j];
+  }
+  HIP_TRY(hipMemcpy(h->exp_buf, v.data(), v.size() * sizeof(R), hipMemcpyHostToDevice));
+  HIP_TRY(hipDeviceSynchronize());
+  S.exp = (const R*)h->exp_buf;
+  return USV_OK;
+}
+
 Handle* as_handle(void* p) { return static_cast<Handle*>(p); }
 
 }  // namespace
@@ -2416,6 +2478,9 @@ int usv_create(const usv_config* cfg, int32_t device, void** out) {
     return fail(USV_ERR_ARG, "unknown autoreset mode");
   if (cfg->lidar_algo != USV_LIDAR_BRUTE && cfg->lidar_algo != USV_LIDAR_WINDOW)
     return fail(USV_ERR_ARG, "unknown lidar algorithm");
+  if ((cfg->flags & ~USV_FLAG_PERTURB) != 0 || cfg->reserved != 0) return fail(USV_ERR_ARG, "unknown flags");
+  if ((cfg->flags & USV_FLAG_PERTURB) && cfg->mode != USV_MODE_ASMC_SIMPLE)
+    return fail(USV_ERR_ARG, "USV_FLAG_PERTURB applies to usv-asmc-simple only");
   int ndev = 0;
   HIP_TRY(hipGetDeviceCount(&ndev));
   if (device < 0 || device >= ndev) return fail(USV_ERR_ARG, "bad device index");
@@ -2438,14 +2503,11 @@ int usv_create(const usv_config* cfg, int32_t device, void** out) {
   if (const char* v = std::getenv("USV_STEP_VARIANT")) {   // "epb,lid[,kind]" tuning override
     int epb = 0, lid = 0, kind = 0;
     const int got = std::sscanf(v, "%d,%d,%d", &epb, &lid, &kind);
-    const bool blk_ok = kind == 0 && (epb == 16 || epb == 32 || epb == 64);
     const bool wave_ok = kind == 1 && (epb == 16 || epb == 32 || epb == 64) && (lid == 0 || lid == 3 || lid == 7);
-    const bool split_ok = ((kind == 2 && (epb == 4 || epb == 8 || epb == 16 || epb == 32)) ||
-                           (kind == 3 && (epb == 1 || epb == 2 || epb == 4 || epb == 8))) &&
-                          (lid == 0 || lid == 3 || lid == 7);
-    const bool queue_ok = (kind == 4 || kind == 5) && (epb == 64 || epb == 128 || epb == 256) && lid == 7 &&
+    const bool split_ok = kind == 2 && (epb == 8 || epb == 16 || epb == 32) && (lid == 0 || lid == 3 || lid == 7);
+    const bool queue_ok = (kind == 4 || kind == 5) && epb == kQE && lid == 7 &&
                           cfg->precision == USV_F32 && cfg->obstacle_cap <= 32;
-    if (got >= 2 && (blk_ok || wave_ok || split_ok || queue_ok) && lid >= 0 && lid <= 7) {
+    if (got >= 3 && (wave_ok || split_ok || queue_ok)) {
       h->epb = epb;
       h->lid = lid;
       h->kind = kind;
@@ -2453,9 +2515,9 @@ int usv_create(const usv_config* cfg, int32_t device, void** out) {
   }
   h->prio = (h->kind == 4 || h->kind == 5) ? 0 : 1;   // the ramp helps static splits only
   if (const char* v = std::getenv("USV_PRIO")) h->prio = std::atoi(v);   // tuning override
-  if (h->kind == 4 || h->kind == 5) {   // the block-queue step's LDS can exceed the 64 KiB default
-    HIP_TRY(hipFuncSetAttribute(pick_q(cfg->mode, h->kind == 5, h->epb), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)lds_q_bytes(cfg->obstacle_cap, q_waves(h->epb), h->epb)));
+  if (h->kind == 4 || h->kind == 5) {   // the block-queue step's LDS exceeds the 64 KiB default
+    HIP_TRY(hipFuncSetAttribute(pick_q(cfg->mode, h->kind == 5), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds_q_bytes()));
   }
   const int rc = cfg->precision == USV_F32 ? carve<float>(h, h->sf) : carve<double>(h, h->sd);
   if (rc != USV_OK) {
@@ -2505,26 +2567,53 @@ int usv_seed(void* hp, uint64_t seed) {
   int32_t* ep = h->cfg.precision == USV_F32 ? h->sf.I(I_EPISODE) : h->sd.I(I_EPISODE);
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemset(ep, 0, (size_t)h->cfg.num_envs * 4));
+  HIP_TRY(hipDeviceSynchronize());     // ordered before launches on any (non-blocking) stream
   return USV_OK;
 }
 
-int usv_reset(void* hp, const uint8_t* mask, float* obs, void* stream) {
+int usv_reset_ex(void* hp, const uint8_t* mask, float* obs, const usv_reset_options* opt, float* info,
+                 void* stream) {
   Handle* h = as_handle(hp);
   if (!h || !obs) return fail(USV_ERR_ARG, "null argument");
+  const int kpath = opt ? opt->place_obstacles_on_path : 0;
+  if (kpath < 0) return fail(USV_ERR_ARG, "place_obstacles_on_path must be >= 0");
+  if (kpath > 0 && is_legacy(h->cfg.mode))
+    return fail(USV_ERR_ARG, "place_obstacles_on_path applies to usv-simple / usv-asmc-simple only");
+  if (kpath > 0 && 29 + kpath > h->cfg.obstacle_cap)
+    return fail(USV_ERR_ARG, "place_obstacles_on_path needs obstacle_cap >= 29 + k (reference draws up to 29)");
   DeviceGuard g(h->device);
   hipStream_t st = (hipStream_t)stream;
-  return h->cfg.precision == USV_F32 ? launch_reset<float>(h, h->sf, mask, obs, st)
-                                     : launch_reset<double>(h, h->sd, mask, obs, st);
+  return h->cfg.precision == USV_F32 ? launch_reset<float>(h, h->sf, mask, obs, kpath, info, st)
+                                     : launch_reset<double>(h, h->sd, mask, obs, kpath, info, st);
 }
 
-int usv_step(void* hp, const float* act, float* obs, void* rew, uint8_t* term, uint8_t* trunc,
-             float* fobs, void* stream) {
+int usv_reset(void* hp, const uint8_t* mask, float* obs, void* stream) {
+  return usv_reset_ex(hp, mask, obs, nullptr, nullptr, stream);
+}
+
+int usv_step_ex(void* hp, const float* act, float* obs, void* rew, uint8_t* term, uint8_t* trunc,
+                float* fobs, float* info, void* stream) {
   Handle* h = as_handle(hp);
   if (!h || !act || !obs || !rew || !term || !trunc) return fail(USV_ERR_ARG, "null argument");
   DeviceGuard g(h->device);
   hipStream_t st = (hipStream_t)stream;
-  return h->cfg.precision == USV_F32 ? launch_step<float>(h, h->sf, act, obs, rew, term, trunc, fobs, st)
-                                     : launch_step<double>(h, h->sd, act, obs, rew, term, trunc, fobs, st);
+  return h->cfg.precision == USV_F32 ? launch_step<float>(h, h->sf, act, obs, rew, term, trunc, fobs, info, st)
+                                     : launch_step<double>(h, h->sd, act, obs, rew, term, trunc, fobs, info, st);
+}
+
+int usv_step(void* hp, const float* act, float* obs, void* rew, uint8_t* term, uint8_t* trunc,
+             float* fobs, void* stream) {
+  return usv_step_ex(hp, act, obs, rew, term, trunc, fobs, nullptr, stream);
+}
+
+int usv_set_experiment(void* hp, const usv_experiment* x) {
+  Handle* h = as_handle(hp);
+  if (!h) return fail(USV_ERR_ARG, "null handle");
+  if (is_legacy(h->cfg.mode)) return fail(USV_ERR_ARG, "custom experiments apply to usv-simple / usv-asmc-simple only");
+  if (x && (x->n_obs < 1 || x->n_obs > h->cfg.obstacle_cap || x->n_obs > 64))
+    return fail(USV_ERR_ARG, "experiment n_obs must be in [1, obstacle_cap]");
+  DeviceGuard g(h->device);
+  return h->cfg.precision == USV_F32 ? set_experiment<float>(h, h->sf, x) : set_experiment<double>(h, h->sd, x);
 }
 
 int usv_field_info(void* hp, int32_t f, int32_t* per_env, int32_t* is_int, const char** name) {

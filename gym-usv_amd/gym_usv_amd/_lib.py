@@ -14,13 +14,21 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 # diagnostic builds (tools/) may point at another in-tree copy of the library
 LIB_PATH = os.environ.get("USV_LIB_PATH", LIB_PATH)
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 MODE_SIMPLE, MODE_ASMC_SIMPLE, MODE_ASMC_V0, MODE_ASMC_YE_INT_V0, MODE_PID_V0 = 0, 1, 2, 3, 4
 F32, F64 = 0, 1
 AUTORESET_SAME_STEP, AUTORESET_DISABLED = 0, 1
 LIDAR_BRUTE, LIDAR_WINDOW = 0, 1
 RESET_PHILOX, RESET_NUMPY_PCG64 = 0, 1
 OBS_DIM, SENSOR_COUNT, ACT_DIM, ASMC_STATE = 143, 128, 2, 16
+FLAG_PERTURB = 1
+# usv_info_key order (include/usv_hip.h): reference info keys (simple_env.py:102-115, 189-199) -> column
+INFO_KEYS = ("x", "y", "psi", "u", "v", "r", "path_x0", "path_y0", "path_x1", "path_y1", "action0",
+             "action1", "ye", "angle_to_target", "ye_reward", "angle_to_target_reward",
+             "delta_action_reward", "delta_action", "velocity_track_reward", "reference_velocity",
+             "reward_velocity", "reference_velocity_error")
+INFO_DIM = len(INFO_KEYS)
+EXP_MAX_OBS = 64
 
 
 class UsvLibError(RuntimeError):
@@ -32,7 +40,19 @@ class UsvConfig(ctypes.Structure):
                 ("precision", ctypes.c_int32), ("num_envs", ctypes.c_int32),
                 ("obstacle_cap", ctypes.c_int32), ("max_episode_steps", ctypes.c_int32),
                 ("autoreset", ctypes.c_int32), ("lidar_algo", ctypes.c_int32),
-                ("seed", ctypes.c_uint64), ("env_id_offset", ctypes.c_uint64)]
+                ("seed", ctypes.c_uint64), ("env_id_offset", ctypes.c_uint64),
+                ("flags", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+class UsvResetOptions(ctypes.Structure):
+    _fields_ = [("place_obstacles_on_path", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+class UsvExperiment(ctypes.Structure):
+    _fields_ = [("n_obs", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("obstacle_x", ctypes.c_double * EXP_MAX_OBS), ("obstacle_y", ctypes.c_double * EXP_MAX_OBS),
+                ("obstacle_r", ctypes.c_double * EXP_MAX_OBS), ("path_start", ctypes.c_double * 2),
+                ("angle", ctypes.c_double), ("position", ctypes.c_double * 3)]
 
 
 # (name, restype, argtypes) for every function in include/usv_hip.h
@@ -50,7 +70,10 @@ SIGNATURES = [
     ("usv_seed", ctypes.c_int, [_vp, _u64]),
     ("usv_set_reset_rng", ctypes.c_int, [_vp, _i32]),
     ("usv_reset", ctypes.c_int, [_vp, _vp, _vp, _vp]),
+    ("usv_reset_ex", ctypes.c_int, [_vp, _vp, _vp, ctypes.POINTER(UsvResetOptions), _vp, _vp]),
+    ("usv_set_experiment", ctypes.c_int, [_vp, ctypes.POINTER(UsvExperiment)]),
     ("usv_step", ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    ("usv_step_ex", ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     ("usv_field_info", ctypes.c_int, [_vp, _i32, ctypes.POINTER(_i32), ctypes.POINTER(_i32),
                                       ctypes.POINTER(ctypes.c_char_p)]),
     ("usv_get_field", ctypes.c_int, [_vp, _i32, _vp, _sz]),

@@ -27,7 +27,9 @@ def sources():
 
 
 def deps():
-    return sources() + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hpp", ".h"))] + \
+    """Every file the build reads: the sources, everything under csrc/ they include (.hpp, .h, .inc)
+    and the public header."""
+    return sources() + [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hpp", ".h", ".inc"))] + \
         [os.path.join(INCLUDE, "usv_hip.h")]
 
 

@@ -23,14 +23,16 @@ class _SingleEnv:
     metadata = {"render_modes": [], "render_fps": 30}
 
     def __init__(self, render_mode=None, options=None, device=0, precision="f32",
-                 max_episode_steps=0, seed=None, reset_rng="philox"):
+                 max_episode_steps=0, seed=None, reset_rng="philox", obstacle_cap=32, perturb=False):
         if render_mode not in (None, "rgb_array"):
             raise NotImplementedError("render_mode 'human' (a pygame window) is out of scope; use 'rgb_array'")
         self.render_mode = render_mode
         self.options = options or {}
         self._venv = UsvVectorEnv(self.env_id, num_envs=1, device=device, precision=precision,
                                   autoreset=False, max_episode_steps=max_episode_steps,
-                                  seed=0 if seed is None else seed, reset_rng=reset_rng)
+                                  seed=0 if seed is None else seed, reset_rng=reset_rng,
+                                  obstacle_cap=obstacle_cap, options=self.options, info=True,
+                                  perturb=perturb)
         self.observation_space = self._venv.single_observation_space
         self.action_space = self._venv.single_action_space
         self._seeded = False
@@ -40,15 +42,27 @@ class _SingleEnv:
             seed = int(np.random.SeedSequence().entropy % (1 << 63))
         if seed is not None:
             self._seeded = True
-        obs, _ = self._venv.reset(seed=seed, options=options)
-        return obs[0].cpu().numpy(), {}
+        obs, info = self._venv.reset(seed=seed, options=options)
+        return obs[0].cpu().numpy(), self._host_info(info)
 
     def step(self, action):
         a = torch.as_tensor(np.asarray(action, dtype=np.float32).reshape(1, self._venv.act_dim),
                             device=self._venv.device)
-        obs, rew, term, trunc, _ = self._venv.step(a)
+        obs, rew, term, trunc, info = self._venv.step(a)
         return (obs[0].cpu().numpy(), float(rew[0].item()), bool(term[0].item()),
-                bool(trunc[0].item()), {})
+                bool(trunc[0].item()), self._host_info(info))
+
+    @staticmethod
+    def _host_info(info):
+        """The reference's info dict for env 0 (simple_env.py:102-115, 189-199): arrays for
+        position / velocity / path_start / path_end, Python floats for the rest."""
+        out = {}
+        for k, v in info.items():
+            if k in ("final_obs", "_final_obs"):
+                continue
+            x = v[0].detach().cpu().numpy().astype(np.float64)
+            out[k] = x if x.ndim else float(x)
+        return out
 
     def render(self):
         """simple_env.py:117-119: an rgb_array frame when render_mode == "rgb_array"."""

@@ -86,7 +86,11 @@ class UsvVectorEnv:
 
     def __init__(self, env_id="usv-simple", num_envs=4096, device=0, seed=0, precision="f32",
                  autoreset=True, max_episode_steps=None, obstacle_cap=32, lidar="window",
-                 env_id_offset=0, reset_rng="philox"):
+                 env_id_offset=0, reset_rng="philox", options=None, info=False, perturb=False):
+        """``options`` are UsvSimpleEnv's constructor options (simple_env.py:10): only
+        ``run_custom_experiment`` / ``experiment`` (:292-300) exist there.  ``info=True`` returns the
+        reference's per-step info keys (simple_env.py:102-115, 189-199) as device tensors.
+        ``perturb=True`` runs usv-asmc-simple's UsvAsmc.compute with do_perturb (usv_asmc.py:184-199)."""
         if env_id not in ENV_SPECS:
             raise ValueError(f"unknown env id {env_id!r}; known: {sorted(ENV_SPECS)}")
         if not torch.cuda.is_available():
@@ -104,6 +108,7 @@ class UsvVectorEnv:
         cfg.lidar_algo = {"brute": _lib.LIDAR_BRUTE, "window": _lib.LIDAR_WINDOW}[lidar]
         cfg.seed = int(seed)
         cfg.env_id_offset = int(env_id_offset)
+        cfg.flags = _lib.FLAG_PERTURB if perturb else 0
         self.cfg = cfg
         h = ctypes.c_void_p()
         with torch.cuda.device(self.device):
@@ -128,11 +133,70 @@ class UsvVectorEnv:
         self._np_seeded = False
         if reset_rng == "numpy":
             _lib.check(self.lib.usv_set_reset_rng(self._h, _lib.RESET_NUMPY_PCG64))
+        self.info_enabled = bool(info) and env_id not in LEGACY_IDS   # the legacy ids return {}
+        self.info_buf = torch.zeros((n, _lib.INFO_DIM), dtype=torch.float32, **kw) if self.info_enabled else None
+        self.options = dict(options or {})
+        unknown = set(self.options) - {"run_custom_experiment", "experiment"}
+        if unknown:
+            raise ValueError(f"unknown constructor options {sorted(unknown)} (UsvSimpleEnv reads only "
+                             "'run_custom_experiment' and 'experiment', simple_env.py:292-300)")
+        if self.options and env_id != "usv-simple":
+            raise ValueError("constructor options exist for usv-simple only (UsvSimpleASMCEnv.__init__ takes "
+                             "none, simple_env_asmc.py:10)")
+        if self.options.get("run_custom_experiment"):
+            self.set_experiment(self.options["experiment"])
+
+    def set_experiment(self, exp):
+        """Install a custom experiment (simple_env.py:292-300) for every env: each reset keeps its
+        draws but takes obstacles, path and pose from ``exp`` (keys obstacle_positions [n,2],
+        obstacle_radius [n], path_start [2], angle, position [3]); ``None`` removes it."""
+        if exp is None:
+            _lib.check(self.lib.usv_set_experiment(self._h, None))
+            return
+        x = _lib.UsvExperiment()
+        pos = np.asarray(exp["obstacle_positions"], dtype=np.float64).reshape(-1, 2)
+        rad = np.asarray(exp["obstacle_radius"], dtype=np.float64).reshape(-1)
+        if pos.shape[0] != rad.shape[0] or not 1 <= pos.shape[0] <= min(self.cfg.obstacle_cap, _lib.EXP_MAX_OBS):
+            raise ValueError(f"experiment needs 1..{self.cfg.obstacle_cap} obstacles with one radius each")
+        x.n_obs = pos.shape[0]
+        for j in range(x.n_obs):
+            x.obstacle_x[j], x.obstacle_y[j], x.obstacle_r[j] = pos[j, 0], pos[j, 1], rad[j]
+        ps = np.asarray(exp["path_start"], dtype=np.float64).reshape(2)
+        x.path_start[0], x.path_start[1] = ps
+        x.angle = float(exp["angle"])
+        p3 = np.asarray(exp["position"], dtype=np.float64).reshape(3)
+        x.position[0], x.position[1], x.position[2] = p3
+        _lib.check(self.lib.usv_set_experiment(self._h, ctypes.byref(x)))
+
+    def _info_dict(self, reset=False):
+        """The reference's info keys as device tensors (views of the info buffer)."""
+        b, n = self.info_buf, self.num_envs
+        col = {k: i for i, k in enumerate(_lib.INFO_KEYS)}
+        d = {"position": b[:, 0:3], "velocity": b[:, 3:6], "path_start": b[:, 6:8], "path_end": b[:, 8:10],
+             "reward": torch.full((n,), -1.0, device=self.device) if reset else self.reward,
+             "action0": b[:, col["action0"]], "action1": b[:, col["action1"]],
+             "left_thruster": torch.zeros(n, device=self.device), "right_thruster": torch.zeros(n, device=self.device),
+             "ye": b[:, col["ye"]], "angle_to_target": b[:, col["angle_to_target"]]}
+        if not reset:
+            for k in ("ye_reward", "angle_to_target_reward", "delta_action_reward", "delta_action",
+                      "velocity_track_reward", "reference_velocity", "reward_velocity", "reference_velocity_error"):
+                d[k] = b[:, col[k]]
+            d["angle_action_reward"] = torch.zeros(n, device=self.device)
+        return d
 
     # ------------------------------------------------------------------ API
     def reset(self, seed=None, options=None, mask=None):
-        if options:
-            raise NotImplementedError("reset options (place_obstacles_on_path) are not supported yet")
+        """UsvSimpleEnv.reset (simple_env.py:228-308) for every env (or those where ``mask``);
+        ``options={'place_obstacles_on_path': k}`` (:276-288) needs ``obstacle_cap >= 29 + k``."""
+        opts = dict(options or {})
+        unknown = set(opts) - {"place_obstacles_on_path"}
+        if unknown:
+            raise ValueError(f"unknown reset options {sorted(unknown)} (simple_env.py:276 reads only "
+                             "'place_obstacles_on_path')")
+        ropt = _lib.UsvResetOptions()
+        # UsvSimpleASMCEnv.reset drops its options (simple_env_asmc.py:14-16: super().reset(seed=seed))
+        if self.env_id == "usv-simple":
+            ropt.place_obstacles_on_path = int(opts.get("place_obstacles_on_path") or 0)
         if self.reset_rng == "numpy":
             # each env owns a numpy Generator(PCG64(SeedSequence(seed_i))), like gymnasium's
             # Env.reset(seed) (simple_env.py:229); an int seed gives env i seed + global id (the
@@ -154,8 +218,9 @@ class UsvVectorEnv:
         m = None
         if mask is not None:
             m = torch.as_tensor(mask, device=self.device).to(torch.uint8).contiguous()
-        _lib.check(self.lib.usv_reset(self._h, _ptr(m), _ptr(self.obs), _stream_ptr(self.device)))
-        return self.obs, {}
+        _lib.check(self.lib.usv_reset_ex(self._h, _ptr(m), _ptr(self.obs), ctypes.byref(ropt),
+                                         _ptr(self.info_buf), _stream_ptr(self.device)))
+        return self.obs, (self._info_dict(reset=True) if self.info_enabled else {})
 
     def step(self, actions):
         a = torch.as_tensor(actions, device=self.device)
@@ -165,12 +230,14 @@ class UsvVectorEnv:
             a = a.reshape(self.num_envs, 1)
         if a.shape != (self.num_envs, self.act_dim):
             raise ValueError(f"actions must be [{self.num_envs}, {self.act_dim}], got {tuple(a.shape)}")
-        _lib.check(self.lib.usv_step(self._h, _ptr(a), _ptr(self.obs), _ptr(self.reward),
-                                     _ptr(self._term), _ptr(self._trunc), _ptr(self.final_obs),
-                                     _stream_ptr(self.device)))
+        _lib.check(self.lib.usv_step_ex(self._h, _ptr(a), _ptr(self.obs), _ptr(self.reward),
+                                        _ptr(self._term), _ptr(self._trunc), _ptr(self.final_obs),
+                                        _ptr(self.info_buf), _stream_ptr(self.device)))
         term = self._term.view(torch.bool)
         trunc = self._trunc.view(torch.bool)
         info = {"final_obs": self.final_obs, "_final_obs": term | trunc}
+        if self.info_enabled:
+            info.update(self._info_dict())
         return self.obs, self.reward, term, trunc, info
 
     def step_raw(self, actions, obs, reward, term, trunc, final_obs=None, stream=None):

@@ -15,6 +15,10 @@
  *                      UsvAsmcEnv.reset (usv_asmc_env.py:258-300),
  *                      UsvAsmcYeIntEnv.reset (usv_asmc_ye_int_env.py:256-296),
  *                      UsvPidEnv.reset (usv_pid_env.py:236-276)
+ *   usv_reset_ex    <- UsvSimpleEnv.reset(options={'place_obstacles_on_path': k}) (:276-288) and
+ *                      its info dict _get_info(-1, zeros(3)) (simple_env.py:102-115, :305)
+ *   usv_set_experiment <- UsvSimpleEnv(options={'run_custom_experiment': ..}) (:10, :292-300)
+ *   usv_step_ex     <- the step's info dict (simple_env.py:102-115, 189-199, 343-344)
  *   usv_step        <- UsvSimpleEnv.step (simple_env.py:310-346),
  *                      UsvSimpleASMCEnv.step (simple_env_asmc.py:18-27) -> UsvAsmc.compute
  *                      (gym_usv/control/usv_asmc.py:53-244), lidar
@@ -44,7 +48,7 @@
 extern "C" {
 #endif
 
-#define USV_ABI_VERSION 1
+#define USV_ABI_VERSION 2
 #define USV_SENSOR_COUNT 128
 #define USV_OBS_DIM 143      /* 15 + 128, simple_env.py:27 */
 #define USV_ACT_DIM 2        /* simple_env.py:30 */
@@ -99,7 +103,55 @@ typedef struct usv_config {
   int32_t lidar_algo;        /* usv_lidar_algo */
   uint64_t seed;             /* Philox key for in-kernel resets */
   uint64_t env_id_offset;    /* global id of env 0 (sharding across GPUs) */
+  int32_t flags;             /* usv_flags */
+  int32_t reserved;          /* 0 */
 } usv_config;
+
+typedef enum usv_flags {
+  /* usv-asmc-simple: UsvAsmc.compute(..., do_perturb=True) (gym_usv/control/usv_asmc.py:184-199):
+     a sinusoidal force is added to the thrust every substep; the controller's perturb_step is
+     20 * elapsed + substep (a fresh UsvAsmc per episode, 2 x 10 substeps per env step) */
+  USV_FLAG_PERTURB = 1
+} usv_flags;
+
+/* Per-step info (opt-in, usv_step_ex / usv_reset_ex): one f32 row of USV_INFO_DIM values per env,
+ * the keys of UsvSimpleEnv._get_info + reward_info (gym_usv/envs/simple_env.py:102-115,189-199).
+ * "reward" is rew_dev itself; keys that are constant in the reference (left/right_thruster = 0,
+ * angle_action_reward = 0) are not stored.  After an explicit reset the row is
+ * _get_info(-1, zeros(3)) (:305): the reward-term entries are 0.  With same-step autoreset the
+ * row of a done env keeps its terminal step's info. */
+typedef enum usv_info_key {
+  USV_INFO_X = 0, USV_INFO_Y, USV_INFO_PSI,      /* 'position' (after the step)            */
+  USV_INFO_U, USV_INFO_V, USV_INFO_R,            /* 'velocity'                             */
+  USV_INFO_PATH_X0, USV_INFO_PATH_Y0,            /* 'path_start'                           */
+  USV_INFO_PATH_X1, USV_INFO_PATH_Y1,            /* 'path_end'                             */
+  USV_INFO_ACTION0, USV_INFO_ACTION1,            /* 'action0', 'action1' (filtered action)  */
+  USV_INFO_YE,                                   /* 'ye'                                   */
+  USV_INFO_ANGLE_TO_TARGET,                      /* 'angle_to_target' (= angle / pi)       */
+  USV_INFO_YE_REWARD, USV_INFO_ANGLE_TO_TARGET_REWARD, USV_INFO_DELTA_ACTION_REWARD,
+  USV_INFO_DELTA_ACTION, USV_INFO_VELOCITY_TRACK_REWARD,
+  USV_INFO_REFERENCE_VELOCITY, USV_INFO_REWARD_VELOCITY, USV_INFO_REFERENCE_VELOCITY_ERROR,
+  USV_INFO_DIM
+} usv_info_key;
+
+/* reset(options=...) of UsvSimpleEnv.reset (simple_env.py:276-288) */
+typedef struct usv_reset_options {
+  int32_t place_obstacles_on_path;  /* k > 0: k extra obstacles scattered along the path;
+                                       needs obstacle_cap >= 29 + k */
+  int32_t reserved;
+} usv_reset_options;
+
+/* __init__(options={'run_custom_experiment': True, 'experiment': {...}}) of UsvSimpleEnv
+ * (simple_env.py:10,292-300): every reset (explicit or autoreset) of every env of the handle
+ * replaces the drawn obstacles, path and pose by these, after the usual draws. */
+typedef struct usv_experiment {
+  int32_t n_obs;               /* 1 .. obstacle_cap */
+  int32_t reserved;
+  double obstacle_x[64], obstacle_y[64], obstacle_r[64];  /* 'obstacle_positions', 'obstacle_radius' */
+  double path_start[2];        /* 'path_start' */
+  double angle;                /* 'angle': path_end = path_start + (cos, sin)(angle) * 100 */
+  double position[3];          /* 'position' (x, y, psi) */
+} usv_experiment;
 
 /* Per-env state fields.  Host-side layout for get/set: [num_envs][per_env] row-major,
  * float64 for real fields, int32 for integer fields (usv_field_info tells which). */
@@ -162,6 +214,12 @@ int usv_set_reset_rng(void* handle, int32_t kind);
 /* Reset envs whose mask byte is non-zero (all envs if mask_dev == NULL) and write their
  * reset observation rows into obs_dev [num_envs][obs_dim] (other rows untouched). */
 int usv_reset(void* handle, const uint8_t* mask_dev, float* obs_dev, void* stream);
+/* usv_reset with reset options (NULL = none) and an optional info buffer info_dev
+ * [num_envs][USV_INFO_DIM] f32 (NULL = none; rows of reset envs are written). */
+int usv_reset_ex(void* handle, const uint8_t* mask_dev, float* obs_dev,
+                 const usv_reset_options* options, float* info_dev, void* stream);
+/* Install (experiment != NULL) or remove (NULL) the custom experiment of every env. */
+int usv_set_experiment(void* handle, const usv_experiment* experiment);
 
 /* One env step for every env.
  *   act_dev       [num_envs][act_dim] f32 (u in [0.2,1], r in [-1,1]; usv-asmc-simple: (u_d, psi
@@ -173,6 +231,11 @@ int usv_reset(void* handle, const uint8_t* mask_dev, float* obs_dev, void* strea
  *                 (rows of envs not done are left untouched). */
 int usv_step(void* handle, const float* act_dev, float* obs_dev, void* rew_dev,
              uint8_t* term_dev, uint8_t* trunc_dev, float* final_obs_dev, void* stream);
+/* usv_step that also writes the per-step info rows into info_dev [num_envs][USV_INFO_DIM] f32
+ * (usv-simple / usv-asmc-simple; the legacy *-v0 ids return {} in the reference and ignore it). */
+int usv_step_ex(void* handle, const float* act_dev, float* obs_dev, void* rew_dev,
+                uint8_t* term_dev, uint8_t* trunc_dev, float* final_obs_dev, float* info_dev,
+                void* stream);
 
 /* Field metadata: values per env, 1 if int32, name. */
 int usv_field_info(void* handle, int32_t field, int32_t* per_env, int32_t* is_int,

@@ -122,15 +122,18 @@ class AsmcBatch:
 
     def __init__(self, n):
         self.state = np.zeros((n, ASMC_N))
+        self.perturb_step = np.zeros(n, dtype=np.int64)                   # usv_asmc.py:49
 
     def reset(self, idx=None):
         if idx is None:
             self.state[:] = 0.0
+            self.perturb_step[:] = 0
         else:
             self.state[idx] = 0.0
+            self.perturb_step[idx] = 0
 
-    def compute(self, action, pos, vel, substeps=10):
-        """usv_asmc.py:53-244 with do_perturb=False. action [N,2] = (u_d, psi offset)."""
+    def compute(self, action, pos, vel, substeps=10, do_perturb=False):
+        """usv_asmc.py:53-244. action [N,2] = (u_d, psi offset)."""
         st = self.state
         a0, a1 = action[:, 0].astype(np.float64), action[:, 1].astype(np.float64)
         x, y, psi = pos[:, 0].copy(), pos[:, 1].copy(), pos[:, 2].copy()
@@ -176,6 +179,16 @@ class AsmcBatch:
             tstbd = tx / (2 * C_TH) - tz / (B_TH * C_TH)                  # :159
             t0 = tport + C_TH * tstbd                                     # :176
             t2 = 0.5 * B_TH * (tport - C_TH * tstbd)
+            t1 = np.zeros_like(t0)
+            if do_perturb:                                                # :184-198, T += F @ J
+                t = self.perturb_step * H
+                k = 10 * (2 * np.pi)
+                fx = np.cos(t * k) * 5
+                fy = np.cos(t + k + 10) * 5
+                cps, sps = np.cos(psi), np.sin(psi)
+                t0 = t0 + (fx * cps + fy * sps)
+                t1 = t1 + (fx * -sps + fy * cps)
+            self.perturb_step = self.perturb_step + 1                     # :199
             # C(nu) = CRB + CA (:201-211), D = Dl - Dn (:213-223); rhs = T - C nu - D nu
             c02 = -MASS * v + 2 * (Y_V_DOT * v + ((Y_R_DOT + N_V_DOT) / 2) * r)
             c12 = MASS * u - X_U_DOT * MASS * u
@@ -187,7 +200,7 @@ class AsmcBatch:
             d21 = -nv - (NVV * np.abs(v) + NVR * np.abs(r))
             d22 = -nr - (NRV * np.abs(v) + NRR * np.abs(r))
             rhs0 = t0 - c02 * r - d00 * u
-            rhs1 = 0.0 - c12 * r - (d11 * v + d12 * r)
+            rhs1 = t1 - c12 * r - (d11 * v + d12 * r)
             rhs2 = t2 - (c20 * u + c21 * v) - (d21 * v + d22 * r)
             ud = M_INV[0, 0] * rhs0 + M_INV[0, 1] * rhs1 + M_INV[0, 2] * rhs2               # :226
             vd = M_INV[1, 0] * rhs0 + M_INV[1, 1] * rhs1 + M_INV[1, 2] * rhs2
@@ -223,8 +236,10 @@ class SimpleEnvBatch:
     obs_dim = OBS_DIM
     act_dim = 2
 
-    def __init__(self, n, cap=32):
+    def __init__(self, n, cap=32, options=None):
         self.n, self.cap = n, cap
+        self.options = dict(options or {})                                # simple_env.py:10,15
+        self.info = {}
         z = lambda *s: np.zeros((n,) + s)
         self.position, self.velocity, self.last_action = z(3), z(3), z(3)
         self.max_action = np.tile(np.array([3.0, 0.0, 3.0]), (n, 1))       # simple_env.py:32
@@ -315,7 +330,7 @@ class SimpleEnvBatch:
             pos = g.uniform(0, BOUND_HI, size=(1, 2))
         if options and options.get("place_obstacles_on_path"):                       # :276-288
             k = options["place_obstacles_on_path"]
-            mag = g.uniform(0, np.hypot(BOUND_HI, BOUND_HI), k)
+            mag = g.uniform(0, np.hypot(0.0, BOUND_HI), k)                # hypot(*env_bounds) = 20
             lx = g.normal(np.cos(angle) * mag + start[0], 1)
             ly = g.normal(np.sin(angle) * mag + start[1], 1)
             pos = np.concatenate([pos, np.stack([lx, ly], axis=1)])
@@ -323,6 +338,14 @@ class SimpleEnvBatch:
         if n > self.cap:
             raise ValueError(f"obstacle count {n} exceeds cap {self.cap}")
         rad = g.uniform(0.15, 0.5, size=n)                                           # :290
+        if self.options.get("run_custom_experiment"):                                # :292-300
+            x = self.options["experiment"]
+            pos = np.asarray(x["obstacle_positions"], dtype=np.float64).reshape(-1, 2)
+            rad = np.asarray(x["obstacle_radius"], dtype=np.float64).reshape(-1)
+            self.path_start[i] = x["path_start"]
+            self.path_end[i] = self.path_start[i] + np.array([np.cos(x["angle"]), np.sin(x["angle"])]) * 100
+            self.position[i] = x["position"]
+            n = pos.shape[0]
         self.n_obs[i] = n
         self.ox[i], self.oy[i], self.orad[i] = 0.0, 0.0, 0.0
         self.ox[i, :n], self.oy[i, :n], self.orad[i, :n] = pos[:, 0], pos[:, 1], rad
@@ -361,8 +384,35 @@ class SimpleEnvBatch:
         truncated = np.any((pxy > BOUND_HI) | (pxy < 0), axis=1)          # :336
         obs = self.obs(self.last_action)                                  # :338 (previous action)
         rew = self.reward(a3)                                             # :339
+        self.info = self.step_info(a3, rew)                               # :341-342
         self.last_action = a3                                             # :343
         return obs, rew, terminated, truncated
+
+    def reset_info(self):
+        """_get_info(-1, zeros(3)) of the reset (:102-115, :305)."""
+        return {"position": self.position.copy(), "velocity": self.velocity.copy(),
+                "path_start": self.path_start.copy(), "path_end": self.path_end.copy(),
+                "reward": np.full(self.n, -1.0), "action0": np.zeros(self.n), "action1": np.zeros(self.n),
+                "ye": self.ye(), "angle_to_target": self.target_state()[:, 0]}
+
+    def step_info(self, a3, rew):
+        """_get_info(reward, action) + reward_info of a step (:102-115, :189-199); ``a3`` is the
+        new filtered action, ``self.last_action`` still the previous one."""
+        info = {"position": self.position.copy(), "velocity": self.velocity.copy(),
+                "path_start": self.path_start.copy(), "path_end": self.path_end.copy(),
+                "reward": rew, "action0": a3[:, 0], "action1": a3[:, 2],
+                "ye": self.ye(), "angle_to_target": self.target_state()[:, 0]}
+        ye = self.ye()
+        k = 0.075
+        delta = np.abs(self.last_action - a3).sum(axis=1)
+        info.update(ye_reward=np.maximum(np.exp(-np.abs(ye / k)), np.exp(-np.power(ye / k, 2))),
+                    angle_to_target_reward=np.exp(-np.abs(self.angle_to_target())),
+                    delta_action_reward=-(delta / 2) * 0.15, delta_action=delta,
+                    velocity_track_reward=np.exp(-np.abs(np.hypot(self.velocity[:, 0], self.velocity[:, 1])
+                                                         - self.ref_v)) * 0.05,
+                    reference_velocity=self.ref_v.copy(), reward_velocity=self.last_action[:, 0].copy(),
+                    reference_velocity_error=self.last_action[:, 0] - self.ref_v)
+        return info
 
     # ---- state exchange with the HIP library (field names = include/usv_hip.h) ----
     def get_state(self):
@@ -384,9 +434,10 @@ class SimpleAsmcEnvBatch(SimpleEnvBatch):
     of 0.01 s) then ``UsvSimpleEnv.step(zeros(2))``.  Reset re-creates the controller
     (zero state) and drops ``options`` (:14-16)."""
 
-    def __init__(self, n, cap=32):
-        super().__init__(n, cap)
+    def __init__(self, n, cap=32, options=None, perturb=False):
+        super().__init__(n, cap, options)
         self.asmc = AsmcBatch(n)
+        self.perturb = perturb           # compute(..., do_perturb) (the reference env passes False)
 
     def reset_env(self, i, seed=None, options=None):
         self.asmc.reset([i])
@@ -395,7 +446,8 @@ class SimpleAsmcEnvBatch(SimpleEnvBatch):
     def step(self, action):
         action = np.asarray(action, dtype=np.float64)
         for _ in range(2):                                                # simple_env_asmc.py:19-25
-            self.position, self.velocity = self.asmc.compute(action, self.position, self.velocity)
+            self.position, self.velocity = self.asmc.compute(action, self.position, self.velocity,
+                                                             do_perturb=self.perturb)
         a3 = self.kinematics(np.zeros((self.n, 2)))                       # :27 super().step(zeros)
         return self._finish_step(a3)
 
@@ -411,9 +463,12 @@ class OracleVectorEnv:
     TimeLimit(max_episode_steps) (gym_usv/__init__.py:24-34) and same-step autoreset
     (``final_obs`` = the terminal obs; the returned obs is the reset obs)."""
 
-    def __init__(self, env_id, num_envs, cap=32):
-        cls = {"usv-simple": SimpleEnvBatch, "usv-asmc-simple": SimpleAsmcEnvBatch}[env_id]
-        self.env = cls(num_envs, cap)
+    def __init__(self, env_id, num_envs, cap=32, options=None, perturb=False):
+        if env_id == "usv-simple":
+            assert not perturb, "do_perturb is usv-asmc-simple's"
+            self.env = SimpleEnvBatch(num_envs, cap, options)
+        else:
+            self.env = SimpleAsmcEnvBatch(num_envs, cap, options, perturb)
         self.limit = TIME_LIMITS[env_id]
         self.elapsed = np.zeros(num_envs, dtype=np.int64)
 

@@ -17,6 +17,16 @@ reference source travels.  Fixtures:
 * ``asmc_ye_int_traj.npz`` / ``pid_traj.npz`` -- the float64 legacy envs UsvAsmcYeIntEnv
                             (usv-asmc-ye-int-v0) and UsvPidEnv (usv-pid-v0), same protocol
                             (``python tests/golden/make_golden.py --legacy-f64`` makes only these).
+
+Round 2 (``--r2`` makes only these):
+
+* ``asmc_perturb_traj.npz`` -- usv-asmc-simple rollouts with UsvAsmc.compute(..., do_perturb=True)
+                            (usv_asmc.py:184-199), plus raw compute() sequences from fresh controllers.
+* ``simple_info_traj.npz``  -- usv-simple rollouts recording the reset / step info dicts
+                            (simple_env.py:102-115, 189-199).
+* ``reset_options.npz``     -- reset(seed, options={'place_obstacles_on_path': k}) (:276-288).
+* ``experiment.npz``        -- UsvSimpleEnv(options={'run_custom_experiment': True, ...}) resets and
+                            rollouts (:292-300).
 """
 from __future__ import annotations
 
@@ -226,9 +236,163 @@ def gen_legacy_f64(E, cls, fname, n_env=4, T=2000, seed0=3000):
     print(fname, "episodes ended:", int(done.sum()))
 
 
+# --------------------------------------------------------------------------- round-2 fixtures
+CAP2 = 64
+
+
+def snapshot64(env):
+    """snapshot() with room for 29 + k obstacles (place_obstacles_on_path)."""
+    n = env.obstacle_n
+    ox, oy, r = np.zeros(CAP2), np.zeros(CAP2), np.zeros(CAP2)
+    ox[:n], oy[:n], r[:n] = env.obstacle_positions[:, 0], env.obstacle_positions[:, 1], env.obstacle_radius
+    return dict(position=np.array(env.position, dtype=np.float64), velocity=np.array(env.velocity, dtype=np.float64),
+                path_start=np.array(env.path_start, dtype=np.float64), path_end=np.array(env.path_end, dtype=np.float64),
+                target=np.array(env.target_position, dtype=np.float64),
+                max_action=np.array(env.max_action, dtype=np.float64), ref_v=float(env.reference_velocity),
+                n_obs=int(n), ox=ox, oy=oy, orad=r)
+
+
+INFO_VEC = ("position", "velocity", "path_start", "path_end")
+INFO_SCALAR = ("reward", "action0", "action1", "ye", "angle_to_target", "ye_reward", "angle_to_target_reward",
+               "delta_action_reward", "delta_action", "velocity_track_reward", "reference_velocity",
+               "reward_velocity", "reference_velocity_error")
+
+
+def gen_asmc_perturb(E, n_env=6, T=160, fname="asmc_perturb_traj.npz"):
+    """usv-asmc-simple with UsvAsmc.compute(..., do_perturb=True) (usv_asmc.py:184-199): the
+    env's step (simple_env_asmc.py:18-27) with the reference's own compute called with the
+    flag set; plus raw compute() sequences from a fresh controller (perturb_step 0, 10, 20, ...)."""
+    from gym_usv.control.usv_asmc import UsvAsmc
+
+    class PerturbedASMCEnv(E.UsvSimpleASMCEnv):
+        def step(self, action):
+            for _ in range(2):
+                self.position, self.velocity, _ = self.asmc.compute(action, self.position, self.velocity, True)
+            return E.UsvSimpleEnv.step(self, np.zeros(2))
+
+    gen_traj(E, PerturbedASMCEnv, fname, 1000, n_env=n_env, T=T)
+    rng = np.random.default_rng(77)
+    seqs, acts = [], []
+    for i in range(8):
+        c = UsvAsmc()
+        pos = np.array([rng.uniform(0, 20), rng.uniform(0, 20), rng.uniform(-3, 3)])
+        vel = np.array([rng.uniform(0, 1.5), rng.uniform(-0.2, 0.2), rng.uniform(-0.5, 0.5)])
+        a = np.array([rng.uniform(0.2, 1.0), rng.uniform(-1, 1)], dtype=np.float32)
+        traj = [np.concatenate([pos, vel])]
+        for k in range(120):
+            pos, vel, _ = c.compute(a, pos, vel, True)
+            traj.append(np.concatenate([pos, vel]))
+        seqs.append(np.stack(traj))
+        acts.append(a.astype(np.float64))
+    d = dict(np.load(os.path.join(HERE, fname)))
+    d.update(compute_seq=np.stack(seqs), compute_act=np.stack(acts))
+    np.savez_compressed(os.path.join(HERE, fname), **d)
+    print(fname, "+ compute sequences", d["compute_seq"].shape)
+
+
+def gen_info_traj(E, n_env=4, T=64, fname="simple_info_traj.npz"):
+    """usv-simple rollouts (as gen_traj, TimeLimit 500) recording the reset and step info dicts
+    (simple_env.py:102-115, 189-199, 305)."""
+    rng = np.random.default_rng(17)
+    acts = np.stack([rng.uniform([0.2, -1], [1, 1], size=(T, 2)) for _ in range(n_env)]).astype(np.float32)
+    seeds = np.arange(n_env) + 5000
+    out = {"obs0": np.zeros((n_env, 143), np.float32), "final_obs": np.zeros((n_env, T, 143), np.float32),
+           "reward": np.zeros((n_env, T)), "terminated": np.zeros((n_env, T), bool),
+           "truncated": np.zeros((n_env, T), bool)}
+    for k in INFO_VEC:
+        n = 3 if k in ("position", "velocity") else 2
+        out["info0_" + k] = np.zeros((n_env, n))
+        out["info_" + k] = np.zeros((n_env, T, n))
+    for k in INFO_SCALAR:
+        out["info_" + k] = np.zeros((n_env, T))
+    for k in ("reward", "action0", "action1", "ye", "angle_to_target"):
+        out["info0_" + k] = np.zeros(n_env)
+    st0 = []
+    for e in range(n_env):
+        env = E.UsvSimpleEnv(render_mode=None)
+        o, inf = env.reset(seed=int(seeds[e]))
+        out["obs0"][e] = o
+        st0.append(snapshot(env))
+        for k in INFO_VEC:
+            out["info0_" + k][e] = inf[k]
+        for k in ("reward", "action0", "action1", "ye", "angle_to_target"):
+            out["info0_" + k][e] = inf[k]
+        for t in range(T):
+            o, r, te, tr, inf = env.step(acts[e, t])
+            out["final_obs"][e, t], out["reward"][e, t] = o, r
+            out["terminated"][e, t], out["truncated"][e, t] = bool(te), bool(tr)
+            for k in INFO_VEC:
+                out["info_" + k][e, t] = inf[k]
+            for k in INFO_SCALAR:
+                out["info_" + k][e, t] = inf[k]
+            if te or tr:
+                break
+    st = {f"init_{k}": np.stack([np.asarray(s[k]) for s in st0]) for k in st0[0]}
+    np.savez_compressed(os.path.join(HERE, fname), seeds=seeds, actions=acts, **out, **st)
+    print(fname, {k: v.shape for k, v in out.items() if k.startswith("info_p")})
+
+
+def gen_reset_options(E, fname="reset_options.npz"):
+    """UsvSimpleEnv.reset(seed, options={'place_obstacles_on_path': k}) (simple_env.py:276-288)."""
+    ks = (3, 8, 20, 35)
+    res = {k: [] for k in ("seed", "k", "obs")}
+    snaps = []
+    for k in ks:
+        for sd in range(6):
+            env = E.UsvSimpleEnv(render_mode=None)
+            o, _ = env.reset(seed=100 + sd, options={"place_obstacles_on_path": k})
+            res["seed"].append(100 + sd)
+            res["k"].append(k)
+            res["obs"].append(o)
+            snaps.append(snapshot64(env))
+    out = {k: np.stack([np.asarray(v) for v in vs]) for k, vs in res.items()}
+    out.update({f"snap_{k}": np.stack([np.asarray(s[k]) for s in snaps]) for k in snaps[0]})
+    np.savez_compressed(os.path.join(HERE, fname), **out)
+    print(fname, out["snap_n_obs"])
+
+
+def gen_experiment(E, fname="experiment.npz", T=40):
+    """UsvSimpleEnv(options={'run_custom_experiment': True, 'experiment': ...}) (simple_env.py:292-300):
+    seeded resets (each keeps its draws, then takes the experiment's obstacles, path and pose) and a
+    short random-action rollout from each."""
+    rng = np.random.default_rng(5)
+    n = 12
+    exp = dict(obstacle_positions=rng.uniform(2, 18, size=(n, 2)), obstacle_radius=rng.uniform(0.15, 0.5, n),
+               path_start=np.array([3.0, 4.0]), angle=0.6, position=np.array([3.2, 3.7, 0.4]))
+    seeds = np.arange(4) + 600
+    acts = rng.uniform([0.2, -1], [1, 1], size=(len(seeds), T, 2)).astype(np.float32)
+    obs0 = np.zeros((len(seeds), 143), np.float32)
+    fobs = np.zeros((len(seeds), T, 143), np.float32)
+    rew = np.zeros((len(seeds), T))
+    term = np.zeros((len(seeds), T), bool)
+    trunc = np.zeros((len(seeds), T), bool)
+    snaps = []
+    for i, sd in enumerate(seeds):
+        env = E.UsvSimpleEnv(render_mode=None, options={"run_custom_experiment": True, "experiment": exp})
+        obs0[i], _ = env.reset(seed=int(sd))
+        snaps.append(snapshot(env))
+        for t in range(T):
+            o, r, te, tr, _ = env.step(acts[i, t])
+            fobs[i, t], rew[i, t], term[i, t], trunc[i, t] = o, r, bool(te), bool(tr)
+            if te or tr:
+                break
+    st = {f"init_{k}": np.stack([np.asarray(s[k]) for s in snaps]) for k in snaps[0]}
+    np.savez_compressed(os.path.join(HERE, fname), seeds=seeds, actions=acts, obs0=obs0, final_obs=fobs,
+                        reward=rew, terminated=term, truncated=trunc,
+                        exp_obstacle_positions=exp["obstacle_positions"], exp_obstacle_radius=exp["obstacle_radius"],
+                        exp_path_start=exp["path_start"], exp_angle=exp["angle"], exp_position=exp["position"], **st)
+    print(fname, "steps until end:", (term | trunc).argmax(axis=1))
+
+
 def main():
     refharness.load_reference()
     import gym_usv.envs as E
+    if "--r2" in sys.argv:              # round-2 fixtures only (existing files untouched)
+        gen_asmc_perturb(E)
+        gen_info_traj(E)
+        gen_reset_options(E)
+        gen_experiment(E)
+        return
     if "--legacy-f64" in sys.argv:      # only the usv-asmc-ye-int-v0 / usv-pid-v0 fixtures
         gen_legacy_f64(E, E.UsvAsmcYeIntEnv, "asmc_ye_int_traj.npz")
         gen_legacy_f64(E, E.UsvPidEnv, "pid_traj.npz", seed0=4000)

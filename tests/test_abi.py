@@ -42,7 +42,8 @@ def test_abi_version_and_defaults(lib):
     assert lib.usv_abi_version() == _lib.ABI_VERSION
     cfg = _lib.UsvConfig()
     lib.usv_config_default(ctypes.byref(cfg), _lib.MODE_SIMPLE, 128)
-    assert (cfg.abi_version, cfg.num_envs, cfg.obstacle_cap, cfg.max_episode_steps) == (1, 128, 32, 500)
+    assert (cfg.abi_version, cfg.num_envs, cfg.obstacle_cap, cfg.max_episode_steps) == (_lib.ABI_VERSION, 128, 32, 500)
+    assert (cfg.flags, cfg.reserved) == (0, 0)
     lib.usv_config_default(ctypes.byref(cfg), _lib.MODE_ASMC_SIMPLE, 8)
     assert cfg.max_episode_steps == 1000          # gym_usv/__init__.py:33
     for mode in (_lib.MODE_ASMC_V0, _lib.MODE_PID_V0, _lib.MODE_ASMC_YE_INT_V0):
@@ -69,6 +70,14 @@ def test_create_rejects_bad_config_without_gpu(lib):
     # null handles are reported, not dereferenced
     assert lib.usv_step(None, None, None, None, None, None, None, None) == -1
     assert lib.usv_reset(None, None, None, None) == -1
+    assert lib.usv_step_ex(None, None, None, None, None, None, None, None, None) == -1
+    assert lib.usv_reset_ex(None, None, None, None, None, None) == -1
+    assert lib.usv_set_experiment(None, None) == -1
+    cfg.abi_version = _lib.ABI_VERSION
+    cfg.flags = 4                                  # unknown flag bit
+    assert lib.usv_create(ctypes.byref(cfg), 0, ctypes.byref(h)) == -1
+    cfg.flags = _lib.FLAG_PERTURB                  # do_perturb is usv-asmc-simple's
+    assert lib.usv_create(ctypes.byref(cfg), 0, ctypes.byref(h)) == -1
 
 
 def test_vector_env_fails_loudly_without_gpu():

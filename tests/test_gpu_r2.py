@@ -1,0 +1,448 @@
+"""Round-2 GPU parity: the reference's lidar scenes through the HIP lidar, the headline config C3 at
+its real size (65 536 envs), do_perturb, the per-step info dict, reset / constructor options, and
+real envs sharded over two processes.  Run on an MI355X: pytest -m gpu.
+
+Fixtures are generated from the reference itself (tests/golden/make_golden.py, ``--r2``).
+Tolerances, fp32 kernel vs the float64 reference: obs atol 1e-5 + rtol 1e-4,
+reward atol 1e-4, lidar rays that flip hit/miss at a grazing edge <= 1e-4 of rays; float64 kernel:
+readings 1e-10, obs to float32 rounding.
+"""
+import os
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import usv_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+F32_OBS_ATOL, F32_OBS_RTOL, F32_REW_ATOL = 1e-5, 1e-4, 1e-4
+
+
+def make(env_id, n, **kw):
+    import gym_usv_amd
+    return gym_usv_amd.make_vec(env_id, n, device=0, **kw)
+
+
+def to_np(*ts):
+    torch.cuda.synchronize()
+    return [t.detach().cpu().numpy() for t in ts]
+
+
+def grazing(px, py, psi, ox, oy, orad, n, k):
+    """|r^2 - perp^2| / r^2 of the nearest-to-grazing obstacle ahead of ray k (reference geometry)."""
+    ang = O.SENSOR_START + k * O.SENSOR_RES + psi
+    dx, dy, r = ox[:n] - px, oy[:n] - py, orad[:n]
+    proj = np.cos(ang) * dx + np.sin(ang) * dy
+    perp = np.sin(ang) * dx - np.cos(ang) * dy
+    rel = np.abs(r * r - perp * perp) / (r * r)
+    return float(np.min(np.where(proj >= 0, rel, np.inf), initial=np.inf))
+
+
+def scene_state(g, cap=32):
+    p = g["pos"]
+    n = p.shape[0]
+    st = {"x": p[:, 0], "y": p[:, 1], "psi": p[:, 2], "u": 0.0, "v": 0.0, "r": 0.0, "last_u": 0.0,
+          "last_r": 0.0, "progress": 0.0, "path_x0": 0.0, "path_y0": 0.0, "path_x1": 100.0, "path_y1": 0.0,
+          "max_u": 3.0, "max_r": 3.0, "ref_v": 1.0, "n_obs": g["n_obs"].astype(np.int32),
+          "elapsed": 1, "scan_valid": 1}
+    for k, f in (("obs_x", "ox"), ("obs_y", "oy"), ("obs_r", "orad")):
+        a = np.zeros((n, cap))
+        a[:, :g[f].shape[1]] = g[f]
+        st[k] = a
+    return st
+
+
+def check_readings(got, g, atol, rtol, label, max_flips):
+    """Compare [scenes, 128] readings (metres) with the reference fixture; mismatches beyond the
+    tolerance must be grazing rays and at most `max_flips`."""
+    ref = g["sensors"]
+    err = np.abs(got - ref)
+    bad = err > atol + rtol * np.abs(ref)
+    for i, k in zip(*np.nonzero(bad)):
+        m = grazing(g["pos"][i, 0], g["pos"][i, 1], g["pos"][i, 2], g["ox"][i], g["oy"][i], g["orad"][i],
+                    int(g["n_obs"][i]), k)
+        assert m < 1e-3, f"{label}: scene {i} ray {k}: {got[i, k]} vs {ref[i, k]} is not a grazing ray ({m:.2e})"
+    ok = ~bad
+    print(f"\n[{label}] max |err| non-grazing {err[ok].max():.3e} m, grazing flips {int(bad.sum())}/{bad.size}, "
+          f"negative readings {int((ref < 0).sum())}, |psi| max {np.abs(g['pos'][:, 2]).max():.1f}")
+    assert int(bad.sum()) <= max_flips, f"{label}: {int(bad.sum())} lidar mismatches"
+
+
+# --------------------------------------------------------------------------- lidar fixture
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_lidar_scenes_reset_scan(golden, precision):
+    """The 256 reference scenes of lidar.npz (boat inside obstacles, |psi| up to 20 rad, poses off
+    the field) through the reset kernel's scan at the current pose (usv_asmc_ca_env.py:411-461):
+    f64 brute lidar, f32 angular-window lidar.  Readings come back unnormalised (sensor_last)."""
+    g = golden("lidar.npz")
+    n = g["pos"].shape[0]
+    env = make("usv-simple", n, precision=precision, autoreset=False)
+    env.set_state(scene_state(g))
+    env.reset()
+    got = env.get_field("sensor_last")
+    if precision == "f64":
+        np.testing.assert_allclose(got, g["sensors"], rtol=0, atol=1e-10)
+        print(f"\n[lidar f64 reset scan] max |err| {np.abs(got - g['sensors']).max():.3e}")
+    else:
+        check_readings(got, g, 1e-3, 1e-4, "lidar f32 reset scan", max(3, got.size // 10000))
+    env.close()
+
+
+@pytest.mark.parametrize("variant,precision,lidar", [
+    (None, "f32", "window"),          # default: fused block-queue step (kind 5)
+    ("128,7,4", "f32", "window"),     # split block-queue step
+    ("16,7,2", "f32", "window"),      # split wave scan
+    ("64,7,1", "f32", "window"),      # fused wave kernel
+    (None, "f32", "brute"),           # brute-force lidar (kind 1, lid 3)
+    (None, "f64", "window"),          # f64 default (brute loop)
+])
+def test_lidar_scenes_step(golden, variant, precision, lidar, monkeypatch):
+    """The same scenes through the step kernels: zero velocity and zero action keep the pose
+    bit-for-bit, so the step's obs row carries the scan of the fixture pose (reading / 100)."""
+    if variant:
+        monkeypatch.setenv("USV_STEP_VARIANT", variant)
+    g = golden("lidar.npz")
+    n = g["pos"].shape[0]
+    env = make("usv-simple", n, precision=precision, lidar=lidar, autoreset=False, max_episode_steps=0)
+    env.set_state(scene_state(g))
+    obs, *_ = env.step(torch.zeros(n, 2, device="cuda"))
+    (obs,) = to_np(obs)
+    got = obs[:, 15:].astype(np.float64) * 100.0
+    if precision == "f64":
+        # readings equal to ~1e-15 (test_lidar_scenes_reset_scan): the float32 obs may differ by 1 ulp
+        np.testing.assert_allclose(obs[:, 15:], (g["sensors"] / 100).astype(np.float32), rtol=0, atol=6e-8)
+    else:
+        check_readings(got, g, 1e-3, 1e-4, f"lidar step {variant or 'default'} {lidar}", max(3, got.size // 10000))
+    env.close()
+
+
+# --------------------------------------------------------------------------- C3 at full size
+def test_c3_full_size_65536():
+    """Config C3 at its real size: 65 536 envs.  (1) oracle states injected into a 4096-env slice,
+    one step checked against the oracle at the C2 tolerances; (2) a 10 000-step random-action
+    rollout checked by properties on the device: finite, in-range obs, the TimeLimit (500) exact,
+    resets happen, terminal-obs headers consistent, reset obs rows on the path (ye = 0)."""
+    N, S = 65536, 4096
+    env = make("usv-simple", N, seed=11)
+    env.reset(seed=11)
+    orc = O.OracleVectorEnv("usv-simple", S)
+    orc.reset(list(range(7000, 7000 + S)))
+    rng = np.random.default_rng(3)
+    for _ in range(20):
+        orc.step(rng.uniform([0.2, -1], [1, 1], size=(S, 2)).astype(np.float32))
+    full = env.get_state()
+    for k, v in orc.env.get_state().items():
+        full[k] = np.array(full[k])
+        full[k][:S] = v
+    full["elapsed"] = np.array(full["elapsed"])
+    full["elapsed"][:S] = orc.elapsed
+    full["scan_valid"] = np.ones(N, np.int32)
+    env.set_state(full)
+    a = rng.uniform([0.2, -1], [1, 1], size=(N, 2)).astype(np.float32)
+    obs, rew, term, trunc, info = env.step(torch.from_numpy(a).cuda())
+    g_obs, g_rew, g_term, g_trunc, g_fobs = to_np(obs, rew, term, trunc, info["final_obs"])
+    o_obs, o_rew, o_term, o_trunc, o_fobs, o_done = orc.step(a[:S])
+    flags_ok = (g_term[:S] == o_term) & (g_trunc[:S] == o_trunc)
+    assert (~flags_ok).sum() <= 2
+    done = g_term[:S] | g_trunc[:S]
+    rows = np.where(done[:, None], g_fobs[:S], g_obs[:S])[flags_ok]
+    ref = o_fobs[flags_ok]
+    hdr_err = np.abs(rows[:, :15] - ref[:, :15])
+    assert (hdr_err <= F32_OBS_ATOL + F32_OBS_RTOL * np.abs(ref[:, :15])).all(), hdr_err.max()
+    sens_bad = np.abs(rows[:, 15:] - ref[:, 15:]) > F32_OBS_ATOL + F32_OBS_RTOL * np.abs(ref[:, 15:])
+    assert sens_bad.mean() <= 1e-4, sens_bad.sum()
+    rerr = np.abs(g_rew[:S][flags_ok] - o_rew[flags_ok])
+    coll_flip = np.abs(rerr - 20) < 1
+    assert rerr[~coll_flip].max() <= F32_REW_ATOL and coll_flip.sum() <= 2
+    print(f"\n[C3 slice] header {hdr_err.max():.2e}, reward {rerr[~coll_flip].max():.2e}, "
+          f"grazing flips {int(sens_bad.sum())}")
+
+    # (2) 10 000-step rollout, properties on the device
+    gen = torch.Generator(device="cuda").manual_seed(5)
+    lo, span = torch.tensor([0.2, -1.0], device="cuda"), torch.tensor([0.8, 2.0], device="cuda")
+    ep_len = torch.from_numpy(env.get_field("elapsed")).cuda().to(torch.int32)
+    ends = torch.zeros((), dtype=torch.int64, device="cuda")
+    tl_ends = torch.zeros((), dtype=torch.int64, device="cuda")
+    bad = torch.zeros((), dtype=torch.int64, device="cuda")
+    const = torch.tensor([0.175, 0.0, 0.3], device="cuda")
+    for t in range(10000):
+        act = torch.rand((N, 2), device="cuda", generator=gen) * span + lo
+        obs, rew, term, trunc, info = env.step(act)
+        ep_len += 1
+        done = term | trunc
+        at_limit = ep_len >= 500
+        bad += (ep_len > 500).sum()                         # TimeLimit never exceeded
+        bad += (at_limit & ~done).sum()                     # ... and hit exactly at 500
+        bad += (~torch.isfinite(obs)).sum() + (~torch.isfinite(rew)).sum()
+        bad += (obs[:, 15:] > 1.0).sum() + (obs[:, 15:] < -0.01).sum()
+        bad += (obs[:, 12:15] != const).sum()
+        bad += ((rew > 2.1) | (rew < -21.5)).sum()     # ye, angle, velocity terms <= 2.05; collision -20
+        fo = info["final_obs"][done]
+        bad += (fo[:, 12:15] != const).sum() + (~torch.isfinite(fo)).sum()
+        bad += (obs[done, 5] != 0).sum()                    # reset obs: boat on the path start
+        ends += done.sum()
+        tl_ends += (at_limit & done).sum()
+        ep_len = torch.where(done, torch.zeros_like(ep_len), ep_len)
+    torch.cuda.synchronize()
+    print(f"[C3 rollout] 10000 x {N} steps: episodes ended {int(ends)}, at the TimeLimit {int(tl_ends)}")
+    assert int(bad) == 0
+    assert int(ends) > N and int(tl_ends) > 0
+    env.close()
+
+
+# --------------------------------------------------------------------------- do_perturb
+def golden_state(g, cap=32):
+    p, v, la, ma = g["init_position"], g["init_velocity"], g["init_last_action"], g["init_max_action"]
+    return {"x": p[:, 0], "y": p[:, 1], "psi": p[:, 2], "u": v[:, 0], "v": v[:, 1], "r": v[:, 2],
+            "last_u": la[:, 0], "last_r": la[:, 2], "progress": g["init_progress"],
+            "path_x0": g["init_path_start"][:, 0], "path_y0": g["init_path_start"][:, 1],
+            "path_x1": g["init_path_end"][:, 0], "path_y1": g["init_path_end"][:, 1],
+            "max_u": ma[:, 0], "max_r": ma[:, 2], "ref_v": g["init_ref_v"],
+            "n_obs": g["init_n_obs"], "obs_x": g["init_ox"], "obs_y": g["init_oy"],
+            "obs_r": g["init_orad"], "sensor_last": g["init_sensors"], "elapsed": 0,
+            "scan_valid": 0, "asmc": 0.0}
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_perturb_golden_replay(golden, precision):
+    """usv-asmc-simple with UsvAsmc.compute(..., do_perturb=True) (usv_asmc.py:184-199) vs the
+    reference's rollouts, from its post-reset state up to each env's first episode end."""
+    g = golden("asmc_perturb_traj.npz")
+    n, T = g["actions"].shape[:2]
+    env = make("usv-asmc-simple", n, precision=precision, autoreset=False, perturb=True)
+    env.set_state(golden_state(g))
+    alive = np.ones(n, bool)
+    hdr, rw = 0.0, 0.0
+    for t in range(T):
+        obs, rew, term, trunc, _ = env.step(torch.from_numpy(g["actions"][:, t]).cuda())
+        obs, rew, term, trunc = to_np(obs, rew, term, trunc)
+        m = alive
+        if not m.any():
+            break
+        hdr = max(hdr, float(np.abs(obs[m, :15] - g["final_obs"][m, t, :15]).max()))
+        rw = max(rw, float(np.abs(rew[m] - g["reward"][m, t]).max()))
+        np.testing.assert_array_equal(term[m], g["terminated"][m, t], err_msg=f"t={t}")
+        np.testing.assert_array_equal(trunc[m], g["truncated"][m, t], err_msg=f"t={t}")
+        alive &= ~(g["terminated"][:, t] | g["truncated"][:, t])
+    print(f"\n[perturb {precision}] max |hdr| err {hdr:.3e}, max |rew| err {rw:.3e}")
+    if precision == "f64":
+        assert hdr <= 2e-6 and rw <= 1e-8
+    else:
+        assert hdr <= 1e-3 and rw <= 1e-2
+    env.close()
+
+
+def test_perturb_off_is_reference_default(golden):
+    """Without the flag the controller is the reference env's (do_perturb=False): the perturbed
+    fixture must NOT be reproduced (the force is really applied), the plain one is (test_gpu_parity)."""
+    g = golden("asmc_perturb_traj.npz")
+    n = g["actions"].shape[0]
+    env = make("usv-asmc-simple", n, precision="f64", autoreset=False, perturb=False)
+    env.set_state(golden_state(g))
+    for t in range(20):
+        obs, *_ = env.step(torch.from_numpy(g["actions"][:, t]).cuda())
+    (obs,) = to_np(obs)
+    assert np.abs(obs[:, :15] - g["final_obs"][:, 19, :15]).max() > 1e-4
+    env.close()
+
+
+# --------------------------------------------------------------------------- info
+INFO_KEYS = ("position", "velocity", "path_start", "path_end", "reward", "action0", "action1", "ye",
+             "angle_to_target", "ye_reward", "angle_to_target_reward", "delta_action_reward", "delta_action",
+             "velocity_track_reward", "reference_velocity", "reward_velocity", "reference_velocity_error")
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_step_info_matches_reference(golden, precision):
+    """info=True: the reference's step info dict (simple_env.py:102-115, 189-199), every key."""
+    g = golden("simple_info_traj.npz")
+    n, T = g["actions"].shape[:2]
+    env = make("usv-simple", n, precision=precision, autoreset=False, info=True)
+    env.set_state(golden_state(g))
+    alive = np.ones(n, bool)
+    worst = {}
+    for t in range(T):
+        obs, rew, term, trunc, info = env.step(torch.from_numpy(g["actions"][:, t]).cuda())
+        torch.cuda.synchronize()
+        assert info["left_thruster"].abs().max() == 0 and info["angle_action_reward"].abs().max() == 0
+        for k in INFO_KEYS:
+            v = info[k].detach().cpu().numpy().astype(np.float64)
+            worst[k] = max(worst.get(k, 0.0), float(np.abs(v[alive] - g["info_" + k][alive, t]).max()))
+        alive &= ~(g["terminated"][:, t] | g["truncated"][:, t])
+        if not alive.any():
+            break
+    print(f"\n[info {precision}] " + ", ".join(f"{k} {v:.1e}" for k, v in worst.items()))
+    tol = 2e-6 if precision == "f64" else 2e-4        # f32 info values are float32 roundings
+    for k, v in worst.items():
+        assert v <= tol * max(1.0, float(np.abs(g["info_" + k]).max())), (k, v)
+    env.close()
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_reset_info_numpy_exact(golden, precision):
+    """reset(seed) in the NumPy-exact mode returns the reference's reset obs and info
+    _get_info(-1, zeros(3)) (simple_env.py:305)."""
+    g = golden("simple_info_traj.npz")
+    n = g["seeds"].shape[0]
+    env = make("usv-simple", n, precision=precision, autoreset=False, info=True, reset_rng="numpy")
+    obs, info = env.reset(seed=[int(s) for s in g["seeds"]])
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(obs.cpu().numpy(), g["obs0"], rtol=0, atol=1e-6 if precision == "f64" else 2e-5)
+    for k in ("position", "velocity", "path_start", "path_end", "reward", "action0", "action1", "ye",
+              "angle_to_target"):
+        v = info[k].detach().cpu().numpy().astype(np.float64)
+        np.testing.assert_allclose(v, g["info0_" + k], rtol=1e-6, atol=2e-6 if precision == "f64" else 2e-5,
+                                   err_msg=k)
+    env.close()
+
+
+# --------------------------------------------------------------------------- reset / constructor options
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_reset_place_obstacles_on_path_numpy_exact(golden, precision):
+    """reset(seed, options={'place_obstacles_on_path': k}) (simple_env.py:276-288): the reference's
+    obstacles (kept + k on the path) and reset obs, k up to 35 (61 obstacles, cap 64)."""
+    g = golden("reset_options.npz")
+    for k in np.unique(g["k"]):
+        idx = np.flatnonzero(g["k"] == k)
+        env = make("usv-simple", len(idx), precision=precision, autoreset=False, reset_rng="numpy", obstacle_cap=64)
+        obs, _ = env.reset(seed=[int(s) for s in g["seed"][idx]], options={"place_obstacles_on_path": int(k)})
+        torch.cuda.synchronize()
+        atol = 1e-12 if precision == "f64" else 2e-5
+        np.testing.assert_array_equal(env.get_field("n_obs"), g["snap_n_obs"][idx])
+        for f, sf in (("obs_x", "snap_ox"), ("obs_y", "snap_oy"), ("obs_r", "snap_orad")):
+            np.testing.assert_allclose(env.get_field(f), g[sf][idx], rtol=0, atol=atol, err_msg=f"k={k} {f}")
+        np.testing.assert_allclose(obs.cpu().numpy()[:, :15], g["obs"][idx, :15], rtol=0,
+                                   atol=1e-6 if precision == "f64" else 2e-5)
+        env.close()
+
+
+def test_reset_place_obstacles_on_path_philox():
+    """Philox resets with k path obstacles: counts, and the k appended obstacles scatter around
+    the path line (N(0, 1) per axis about points on it) within 6 sigma."""
+    n, k = 2048, 8
+    env = make("usv-simple", n, obstacle_cap=40, autoreset=False)
+    env.reset(seed=3, options={"place_obstacles_on_path": k})
+    nob = env.get_field("n_obs")
+    assert ((nob >= 1 + k) & (nob <= 29 + k)).all()
+    ox, oy = env.get_field("obs_x"), env.get_field("obs_y")
+    x0, y0, x1, y1 = (env.get_field(f) for f in ("path_x0", "path_y0", "path_x1", "path_y1"))
+    dx, dy = x1 - x0, y1 - y0
+    ln = np.hypot(dx, dy)
+    rows = np.arange(n)[:, None]
+    cols = nob[:, None] - k + np.arange(k)[None, :]
+    px, py = ox[rows, cols] - x0[:, None], oy[rows, cols] - y0[:, None]
+    dist = np.abs(px * dy[:, None] - py * dx[:, None]) / ln[:, None]
+    along = (px * dx[:, None] + py * dy[:, None]) / ln[:, None]
+    assert dist.max() < 6 and (along > -6).all() and (along < 26).all()
+    assert abs(np.mean(along) - 10) < 0.5            # U(0, 20) magnitudes
+    with pytest.raises(Exception):
+        make("usv-simple", 4, obstacle_cap=32).reset(options={"place_obstacles_on_path": 8})  # 29 + 8 > 32
+    env.close()
+
+
+def experiment_of(g):
+    return dict(obstacle_positions=g["exp_obstacle_positions"], obstacle_radius=g["exp_obstacle_radius"],
+                path_start=g["exp_path_start"], angle=float(g["exp_angle"]), position=g["exp_position"])
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_custom_experiment_numpy_exact(golden, precision):
+    """UsvSimpleEnv(options={'run_custom_experiment': True, 'experiment': ...}) (simple_env.py:292-300):
+    seeded resets and rollouts equal the reference's."""
+    g = golden("experiment.npz")
+    n, T = g["actions"].shape[:2]
+    env = make("usv-simple", n, precision=precision, autoreset=False, reset_rng="numpy",
+               options={"run_custom_experiment": True, "experiment": experiment_of(g)})
+    obs, _ = env.reset(seed=[int(s) for s in g["seeds"]])
+    (obs,) = to_np(obs)
+    tol = 1e-6 if precision == "f64" else 2e-5
+    np.testing.assert_allclose(obs[:, :15], g["obs0"][:, :15], rtol=0, atol=tol)
+    np.testing.assert_array_equal(env.get_field("n_obs"), g["init_n_obs"])
+    np.testing.assert_allclose(env.get_field("x"), g["init_position"][:, 0], atol=1e-6)
+    np.testing.assert_allclose(env.get_field("path_x1"), g["init_path_end"][:, 0], atol=1e-5)
+    alive = np.ones(n, bool)
+    for t in range(T):
+        obs, rew, term, trunc, _ = env.step(torch.from_numpy(g["actions"][:, t]).cuda())
+        obs, rew, term, trunc = to_np(obs, rew, term, trunc)
+        np.testing.assert_allclose(obs[alive, :15], g["final_obs"][alive, t, :15], rtol=1e-4,
+                                   atol=tol if precision == "f64" else 1e-4)
+        np.testing.assert_allclose(rew[alive], g["reward"][alive, t], atol=1e-8 if precision == "f64" else 1e-3)
+        alive &= ~(term | trunc)
+    env.close()
+
+
+def test_custom_experiment_autoreset_philox(golden):
+    """Same-step autoresets (Philox) of a handle with an experiment take its obstacles, path and pose."""
+    g = golden("experiment.npz")
+    x = experiment_of(g)
+    n = 512
+    env = make("usv-simple", n, max_episode_steps=4, options={"run_custom_experiment": True, "experiment": x})
+    env.reset(seed=1)
+    for _ in range(9):                         # ends at steps 4 and 8 (TimeLimit) at the latest
+        env.step(torch.rand(n, 2, device="cuda") * torch.tensor([0.8, 2.0], device="cuda")
+                 + torch.tensor([0.2, -1.0], device="cuda"))
+    torch.cuda.synchronize()
+    el = env.get_field("elapsed")
+    fresh = el == 1                            # reset at step 8, stepped once since
+    assert fresh.any()
+    m = len(x["obstacle_radius"])
+    assert (env.get_field("n_obs") == m).all()
+    np.testing.assert_allclose(env.get_field("obs_x")[:, :m], np.broadcast_to(x["obstacle_positions"][:, 0], (n, m)),
+                               atol=1e-5)
+    np.testing.assert_allclose(env.get_field("path_x0"), x["path_start"][0], atol=1e-6)
+    env.close()
+
+
+def test_constructor_options_validated():
+    with pytest.raises(ValueError):
+        make("usv-simple", 4, options={"no_such_option": 1})
+    with pytest.raises(ValueError):
+        make("usv-simple", 4).reset(options={"no_such_option": 1})
+
+
+# --------------------------------------------------------------------------- sharding, two processes
+def _shard_worker(rank, world, tmp, n, steps):
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method=f"file://{tmp}/store", rank=rank, world_size=world)
+    import gym_usv_amd
+    env = gym_usv_amd.make_vec("usv-simple", n, device=0, seed=21, env_id_offset=rank * n, max_episode_steps=30)
+    env.reset(seed=21)
+    gen = torch.Generator().manual_seed(99)
+    outs = []
+    for t in range(steps):
+        a = torch.rand((world * n, 2), generator=gen) * torch.tensor([0.8, 2.0]) + torch.tensor([0.2, -1.0])
+        obs, rew, term, trunc, info = env.step(a[rank * n:(rank + 1) * n].cuda())
+        outs.append(torch.cat([obs.flatten(), rew, term.float(), trunc.float(), info["final_obs"].flatten()]).cpu())
+    out = torch.stack(outs)
+    chk = torch.tensor([float(out.double().sum())])
+    dist.all_reduce(chk)                       # the gloo collective path (checksum of checksums)
+    torch.save({"out": out, "chk": chk}, os.path.join(tmp, f"rank{rank}.pt"))
+    env.close()
+    dist.destroy_process_group()
+
+
+def test_two_process_sharding_bit_identical():
+    """Two processes (gloo) on the one GPU, each stepping n envs with env_id_offset = r * n, equal
+    the single-process 2n-env run bit for bit (DESIGN.md 'Multi-GPU': no step-path collective)."""
+    import torch.multiprocessing as mp
+    n, steps, world = 256, 60, 2
+    with tempfile.TemporaryDirectory() as tmp:
+        mp.start_processes(_shard_worker, args=(world, tmp, n, steps), nprocs=world, join=True, start_method="spawn")
+        parts = [torch.load(os.path.join(tmp, f"rank{r}.pt"), weights_only=True) for r in range(world)]
+    env = make("usv-simple", world * n, seed=21, max_episode_steps=30)
+    env.reset(seed=21)
+    gen = torch.Generator().manual_seed(99)
+    for t in range(steps):
+        a = torch.rand((world * n, 2), generator=gen) * torch.tensor([0.8, 2.0]) + torch.tensor([0.2, -1.0])
+        obs, rew, term, trunc, info = env.step(a.cuda())
+        for r in range(world):
+            sl = slice(r * n, (r + 1) * n)
+            want = torch.cat([obs[sl].flatten(), rew[sl], term[sl].float(), trunc[sl].float(),
+                              info["final_obs"][sl].flatten()]).cpu()
+            assert torch.equal(parts[r]["out"][t], want), f"rank {r} differs at step {t}"
+    total = sum(float(p["out"].double().sum()) for p in parts)
+    assert abs(float(parts[0]["chk"]) - total) <= 1e-6 * abs(total)
+    env.close()

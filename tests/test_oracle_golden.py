@@ -126,3 +126,92 @@ def test_legacy_f64_trajectories_match_reference(golden, fname, family):
             o.reset(idx=idx)
             np.testing.assert_array_equal(o.state[idx].astype(np.float32), g["obs"][idx, t])
     assert g["done"].sum() >= 2
+
+
+# --------------------------------------------------------------------------- round-2 fixtures
+def test_asmc_perturb_compute_matches_reference(golden):
+    """UsvAsmc.compute(..., do_perturb=True) (usv_asmc.py:184-199) from fresh controllers:
+    120 consecutive calls (perturb_step 0, 10, ..., 1190)."""
+    g = golden("asmc_perturb_traj.npz")
+    seq, act = g["compute_seq"], g["compute_act"]
+    a = O.AsmcBatch(seq.shape[0])
+    pos, vel = seq[:, 0, :3].copy(), seq[:, 0, 3:].copy()
+    for k in range(1, seq.shape[1]):
+        pos, vel = a.compute(act, pos, vel, do_perturb=True)
+        # chaotic sign() switches amplify last-bit differences late in the sequence
+        tol = 1e-9 if k <= 40 else 1e-6
+        np.testing.assert_allclose(np.concatenate([pos, vel], axis=1), seq[:, k], rtol=tol, atol=tol,
+                                   err_msg=f"call {k}")
+    assert np.all(a.perturb_step == 10 * (seq.shape[1] - 1))
+
+
+def test_asmc_perturb_trajectories_match_reference(golden):
+    g = golden("asmc_perturb_traj.npz")
+    n, T = g["actions"].shape[:2]
+    venv = O.OracleVectorEnv("usv-asmc-simple", n, perturb=True)
+    obs = venv.reset([int(s) for s in g["seeds"]])
+    np.testing.assert_allclose(obs, g["obs0"], rtol=1e-6, atol=1e-6)
+    for t in range(T):
+        obs, rew, term, trunc, fobs, done = venv.step(g["actions"][:, t])
+        np.testing.assert_array_equal(term, g["terminated"][:, t], err_msg=f"t={t}")
+        np.testing.assert_array_equal(trunc, g["truncated"][:, t], err_msg=f"t={t}")
+        np.testing.assert_allclose(rew, g["reward"][:, t], rtol=1e-8, atol=1e-8, err_msg=f"t={t}")
+        np.testing.assert_allclose(fobs, g["final_obs"][:, t], rtol=1e-6, atol=1e-6, err_msg=f"t={t}")
+        np.testing.assert_allclose(obs, g["obs"][:, t], rtol=1e-6, atol=1e-6, err_msg=f"t={t}")
+
+
+def test_step_and_reset_info_match_reference(golden):
+    """The info dicts of reset and step (simple_env.py:102-115, 189-199), every key."""
+    g = golden("simple_info_traj.npz")
+    n, T = g["actions"].shape[:2]
+    e = O.SimpleEnvBatch(n)
+    e.reset(seeds=[int(s) for s in g["seeds"]])
+    inf = e.reset_info()
+    for k in ("position", "velocity", "path_start", "path_end", "reward", "action0", "action1", "ye",
+              "angle_to_target"):
+        np.testing.assert_allclose(inf[k], g["info0_" + k], rtol=1e-12, atol=1e-12, err_msg=k)
+    alive = np.ones(n, bool)
+    for t in range(T):
+        e.step(g["actions"][:, t])
+        for k, v in e.info.items():
+            np.testing.assert_allclose(v[alive], g["info_" + k][alive, t], rtol=1e-9, atol=1e-9,
+                                       err_msg=f"{k} t={t}")
+        alive &= ~(g["terminated"][:, t] | g["truncated"][:, t])
+        if not alive.any():
+            break
+
+
+def test_reset_place_obstacles_on_path_matches_reference(golden):
+    g = golden("reset_options.npz")
+    for i in range(len(g["seed"])):
+        e = O.SimpleEnvBatch(1, cap=64)
+        obs = e.reset(seeds=[int(g["seed"][i])], options={"place_obstacles_on_path": int(g["k"][i])})
+        np.testing.assert_allclose(obs[0], g["obs"][i], rtol=1e-6, atol=1e-6)
+        assert e.n_obs[0] == g["snap_n_obs"][i]
+        np.testing.assert_allclose(e.ox[0], g["snap_ox"][i], atol=1e-12)
+        np.testing.assert_allclose(e.oy[0], g["snap_oy"][i], atol=1e-12)
+        np.testing.assert_allclose(e.orad[0], g["snap_orad"][i], atol=1e-12)
+        np.testing.assert_allclose(e.position[0], g["snap_position"][i], atol=1e-12)
+
+
+def experiment_of(g):
+    return dict(obstacle_positions=g["exp_obstacle_positions"], obstacle_radius=g["exp_obstacle_radius"],
+                path_start=g["exp_path_start"], angle=float(g["exp_angle"]), position=g["exp_position"])
+
+
+def test_custom_experiment_matches_reference(golden):
+    """UsvSimpleEnv(options={'run_custom_experiment': True, 'experiment': ...}) (simple_env.py:292-300)."""
+    g = golden("experiment.npz")
+    n, T = g["actions"].shape[:2]
+    e = O.SimpleEnvBatch(n, options={"run_custom_experiment": True, "experiment": experiment_of(g)})
+    obs = e.reset(seeds=[int(s) for s in g["seeds"]])
+    np.testing.assert_allclose(obs, g["obs0"], rtol=1e-6, atol=1e-6)
+    np.testing.assert_allclose(e.position, g["init_position"], atol=1e-12)
+    np.testing.assert_allclose(e.path_end, g["init_path_end"], atol=1e-12)
+    np.testing.assert_array_equal(e.n_obs, g["init_n_obs"])
+    alive = np.ones(n, bool)
+    for t in range(T):
+        o, r, te, tr = e.step(g["actions"][:, t])
+        np.testing.assert_allclose(o[alive], g["final_obs"][alive, t], rtol=1e-6, atol=1e-6)
+        np.testing.assert_allclose(r[alive], g["reward"][alive, t], rtol=1e-9, atol=1e-9)
+        alive &= ~(te | tr)
