@@ -725,14 +725,14 @@ constexpr double kStartC = -0.5, kStartS = -0.86602540378443865;                
 // obstacle is ~100 m away).
 template <typename R> struct Scan { R rd0, rd1; bool term, far; };
 
-// |atan2(y, x)| error < 2e-5 rad (minimax on [0,1] + octant folding); only used to size the
-// conservative ray windows, never for a reading.
+// |atan2(y, x)| error < 7e-4 rad = 0.02 ray (degree-5 minimax on [0,1] + octant folding), well inside
+// the quarter-ray window margin; only used to size the conservative ray windows, never for a reading.
 __device__ __forceinline__ float fast_atan2(float y, float x) {
   const float ax = fabsf(x), ay = fabsf(y);
   const float mx = fmaxf(fmaxf(ax, ay), 1e-30f), mn = fminf(ax, ay);
   const float t = mn * __builtin_amdgcn_rcpf(mx);
   const float s = t * t;
-  float p = fmaf(fmaf(fmaf(fmaf(0.0208351f, s, -0.085133f), s, 0.180141f), s, -0.3302995f), s, 0.999866f) * t;
+  float p = fmaf(fmaf(0.0793406442f, s, -0.288691819f), s, 0.995358229f) * t;
   p = ay > ax ? 1.57079633f - p : p;
   p = x < 0.0f ? 3.14159265f - p : p;
   return y < 0.0f ? -p : p;
@@ -743,6 +743,10 @@ __device__ __forceinline__ unsigned ord_key(float k) {   // float -> order-prese
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }
 
+// Exclusive prefix from an inclusive one: the value of lane l - 1 (DPP wave_shr:1; lane 0 gets 0).
+__device__ __forceinline__ int wave_excl_of(int incl) {
+  return __builtin_amdgcn_update_dpp(0, incl, 0x138, 0xF, 0xF, true);
+}
 // Inclusive prefix sum over the 64 lanes (DPP row scans + row carries).
 __device__ __forceinline__ int wave_incl_scan(int v) {
   v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, true);   // row_shr:1
@@ -930,24 +934,29 @@ __device__ __forceinline__ void lidar_window2(float dx, float dy, float key, flo
   const int len1 = valid ? max(0, hi1 - lo1 + 1) : 0, len2 = valid ? max(0, hi2 - lo2 + 1) : 0;
   const int cnt = len1 + len2;
   const int incl = wave_incl_scan(cnt);
-  const int off = incl - cnt;
+  const int off = wave_excl_of(incl);
   const int W = __builtin_amdgcn_readlane(incl, 63);
-  const int meta = lo1 | (len1 << 8) | (lo2 << 16);
+  // Segment marks.  Window w (0, 1) of obstacle lane l is a run of pairs starting at o_w (off, then
+  // off + len1) that maps pair q to ray q + (lo_w - o_w).  Its mark, written at o_w, is
+  // (2 l + w + 1) << 16 | (lo_w - o_w + 32768): the segment id in the high bits keeps the max-scan in
+  // segment order and the ray offset rides in the low bits, so a pair finds its owner obstacle and
+  // its ray from one max-scan, with no per-pair gather of the owner's window.
+  const int o2 = off + len1;
+  const int m1 = ((2 * l + 1) << 16) | (lo1 - off + 32768);
+  const int m2 = ((2 * l + 2) << 16) | (lo2 - o2 + 32768);
   rec[l] = make_float4(a, b, rr * rr, __uint_as_float(ord_key(key)));
-  int carry = 0;                                      // owner marks are lane + 1; 0 = none
+  int carry = 0;
   for (int base = 0; base < W; base += kWave) {       // wave-uniform pass count
     L.mark[l] = 0;
-    if (cnt > 0 && off >= base && off < base + kWave) L.mark[off - base] = l + 1;
+    if (len1 > 0 && off >= base && off < base + kWave) L.mark[off - base] = m1;
+    if (len2 > 0 && o2 >= base && o2 < base + kWave) L.mark[o2 - base] = m2;
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");   // marks and records visible
     __builtin_amdgcn_wave_barrier();
-    const int j1 = max(wave_incl_max(L.mark[l]), carry);
-    carry = __builtin_amdgcn_readlane(j1, 63);
-    const int jj = max(j1 - 1, 0);
+    const int mk = max(wave_incl_max(L.mark[l]), carry);
+    carry = __builtin_amdgcn_readlane(mk, 63);
     const int q = base + l;
-    const int k = q - __shfl(off, jj, kWave);
-    const int mj = __shfl(meta, jj, kWave);
-    const int l1 = mj & 255, n1 = (mj >> 8) & 255, l2 = mj >> 16;
-    const int i = min(max((k < n1 ? l1 : l2 - n1) + k, 0), 127);
+    const int jj = max(((mk >> 16) - 1) >> 1, 0);     // owner obstacle lane
+    const int i = min(max(q + (mk & 0xffff) - 32768, 0), 127);
     const float4 o = rec[jj];                         // owner's (a, b, r^2, key bits)
     const float2 cs = L.rayoff[i];
     const float proj = fmaf(o.x, cs.x, o.y * cs.y);
@@ -1477,8 +1486,13 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
       float hdr[kHdr];
       float px, py, sp, cp, partial;
       bool trunc;
+#ifdef USV_ABL_NODYN     // diagnostic ablation only: pose from x, y, action; no dynamics
+      px = S.F(F_X)[e]; py = S.F(F_Y)[e]; sp = a.x; cp = a.y; partial = 0.0f; trunc = false;
+      for (int i = 0; i < kHdr; ++i) hdr[i] = px;
+#else
       env_dynamics<float, MODE>(S, e, a.x, a.y, hdr, px, py, sp, cp, partial, trunc,
                                 io.info ? io.info + (size_t)e * USV_INFO_DIM : nullptr);
+#endif
       io.trunc[e] = trunc;
       make_qrec(recs + k * kQRec, px, py, sp, cp, partial, S.I(I_NOBS)[e], trunc, hdr);
     }
@@ -1497,6 +1511,16 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
   // a done env and re-entered): inside it their registers would spill the loop's to scratch
   int it = 0;
   const bool hb = l >= 32;
+  // obs-header lanes (loop-invariant, packed in one register): lanes 0..14 store env A's header
+  // value hi, 15..29 env B's, 30..63 repeat lane 29; the record slot of value hi (qrec_hdr) in bits
+  // 8..12, bit 16: env B's lane, bit 17: a constant entry (1, 10, 12, 13, 14)
+  int hpk;
+  {
+    const int hl = min(l, 2 * kHdr - 1);
+    const int hi = hl >= kHdr ? hl - kHdr : hl;
+    const int hrec = hi == 0 ? 6 : (hi <= 9 ? hi + 5 : 15);
+    hpk = hi | (hrec << 8) | ((hl >= kHdr) << 16) | ((hi == 1 || hi == 10 || hi >= 12) << 17);
+  }
   for (;;) {
     unsigned done = 0;
     int de0 = 0;
@@ -1518,8 +1542,13 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
       const float4 meta = *reinterpret_cast<const float4*>(rk + 4);
       const int nt = __float_as_int(meta.y);
       Scan<float> sa, sb;
+#ifdef USV_ABL_NOLIDAR   // diagnostic ablation only: readings from the row and pose, no scan
+      sa.rd0 = cbuf[l & 31] + pose.x; sa.rd1 = pose.y + pose.z; sa.term = sa.far = false;
+      sb = sa;
+#else
       lidar_wave2(cbuf, os, (hb && !hasB) ? 0 : (nt & 0xffff), pose.x, pose.y, pose.z, pose.w, rayoff, slot,
                   mark, sa, sb);
+#endif
       // env B's outputs (env A's again when there is none: identical stores to the same addresses
       // keep every memory instruction of the loop non-divergent and its count static)
       const int eB = hasB ? e0 + 1 : e0;
@@ -1529,16 +1558,19 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
       const bool termB = hasB ? sb.term : sa.term;
       float* const rowA = io.obs + (size_t)e0 * kObsDim;
       float* const rowB = io.obs + (size_t)eB * kObsDim;
+#ifndef USV_ABL_NOSTORE   // (diagnostic ablation: obs rows not written)
       rowA[kHdr + l] = l_norm(sa.rd0);                  // sensors (:82-83)
       rowA[kHdr + 64 + l] = l_norm(sa.rd1);
       rowB[kHdr + l] = l_norm(sB0);
       rowB[kHdr + 64 + l] = l_norm(sB1);
       {                                                 // headers: lanes 0..14 env A, 15..29 env B
-        const int hl = min(l, 2 * kHdr - 1);
-        const bool hB = hl >= kHdr && hasB;
-        const int hi = hl >= kHdr ? hl - kHdr : hl;
-        (hB ? rowB : rowA)[hi] = qrec_hdr(recs + (hB ? k0 + 1 : k0) * kQRec, hi);
+        const int hi = hpk & 31;
+        const bool hB = ((hpk >> 16) & 1) && hasB;      // (no env B: env A's value again)
+        const float hv = recs[(hB ? k0 + 1 : k0) * kQRec + ((hpk >> 8) & 31)];
+        const float hc = hi == 12 ? (float)(kMaxAccU / 10.0) : hi == 14 ? (float)(kMaxAccR / 10.0) : 0.0f;
+        rowA[(hB ? kObsDim : 0) + hi] = ((hpk >> 17) & 1) ? hc : hv;
       }
+#endif
       const bool term_l = hb ? termB : sa.term;         // reward, terminated: lanes 0..31 env A,
       const bool coll_l = hb ? collB : collA;           // 32..63 env B
       io.rew[eb + kl] = coll_l ? -20.0f + meta.x : meta.x;
@@ -1551,7 +1583,11 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
       }
       // the next pair's rows landed: at least seven stores (four sensor halves, the headers, the
       // rewards and the terminated flags) were issued after their DMA
+#ifdef USV_ABL_NOSTORE
+      vm_wait<2>();
+#else
       vm_wait<7>();
+#endif
       cur = nxt;
       if (S.autoreset == USV_AUTORESET_SAME_STEP && (doneA | doneB)) {
         done = (doneA ? 1u : 0u) | (doneB ? 2u : 0u);
@@ -1567,6 +1603,7 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
     }
   }
   USV_STAMP_W(3);
+  USV_STAMP_W(6);
 }
 
 template <int MODE, bool FUSED>

@@ -95,6 +95,25 @@ def main():
     blk = st[: (nw // wpb) * wpb, 4].reshape(-1, wpb)
     out["block_end_spread_us"] = pct(blk.max(1) - blk.min(1))
     out["block_end_us"] = pct(blk.max(1))
+    # co-residency: the blocks that ran on each CU, their start / end, and which one is younger
+    if len(v) > 2 and v[2] in ("4", "5"):
+        blk_id = np.arange(nw) // wpb
+        cu_id = (xcc * 8 + se) * 16 + cu
+        per_cu = {}
+        for b in np.unique(blk_id[: (nw // wpb) * wpb]):
+            m = blk_id == b
+            per_cu.setdefault(int(cu_id[m][0]), []).append((float(st[m, 0].min()), float(st[m, 4].max()), int(b)))
+        pairs = [sorted(x) for x in per_cu.values() if len(x) == 2]
+        out["cus"] = len(per_cu)
+        out["blocks_per_cu"] = pct([len(x) for x in per_cu.values()])
+        if pairs:
+            older_end = np.array([p[0][1] for p in pairs])
+            younger_end = np.array([p[1][1] for p in pairs])
+            out["older_block_start_end_us"] = [round(float(np.mean([p[0][0] for p in pairs])), 2), pct(older_end)]
+            out["younger_block_start_end_us"] = [round(float(np.mean([p[1][0] for p in pairs])), 2), pct(younger_end)]
+            out["younger_has_larger_block_id"] = round(float(np.mean([p[1][2] > p[0][2] for p in pairs])), 3)
+            out["younger_id_ge_half_grid"] = round(float(np.mean([p[1][2] >= nw // wpb // 2 for p in pairs])), 3)
+            out["older_ends_first"] = round(float(np.mean(older_end <= younger_end)), 3)
     print(json.dumps(out))
 
 
