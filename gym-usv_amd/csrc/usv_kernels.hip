@@ -913,49 +913,48 @@ __device__ __forceinline__ void lidar_window(float dx, float dy, float key, floa
 // written after every lane's row reads, which the wave's LDS instructions complete in order),
 // and each pair reads its owner's record: no pose select, no rotation and no re-read of the row.
 // Each lane brings its own env's ray-0 direction (c0r, s0r) = (cos, sin)(psi - 120 deg).
-template <bool RANGE_CHECK>
-__device__ __forceinline__ void lidar_window2(float dx, float dy, float key, float d, float rr, bool valid,
+// One ray window per obstacle: phi is taken in [-32.5, 159.5) rays from ray 0, i.e. with the branch
+// cut in the middle of the rear blind sector (rays cover [0, 127], the blind sector (127, 192)), so a
+// window of half-width < 32.5 rays never wraps onto the rays; wider ones (an obstacle closer than
+// r / sin(61 deg), or the boat inside it) take all 128 rays, the exact test sorting them out.
+// `far` (wave-uniform): some obstacle is >= 99 m away, where the reference's `< max range` test
+// (usv_asmc_ca_env.py:458) can matter; it is applied to every pair then.
+__device__ __forceinline__ void lidar_window2(float dx, float dy, float key, float d, float rr, bool valid, bool far,
                                               float c0r, float s0r, float4* rec, const WinLds& L,
                                               Scan<float>& A, Scan<float>& B) {
   const int l = lane_id();
   float a, b;
   to_ray0(dx, dy, c0r, s0r, a, b);
-  const float phi = fast_atan2(b, a);                 // CCW angle from ray 0; ray i at i*res
-  const float margin = (float)(0.25 * kRes);          // see lidar_window
-  const bool inside = d <= rr * 1.001f;
-  const float x = fminf(rr * __builtin_amdgcn_rcpf(d), 1.0f);
-  const float half = inside ? (float)(kPi / 2) + margin
-                            : fmaf((float)(kPi / 2 - 1) * x, x * x, x) + margin;
   const float inv = (float)(1.0 / kRes);
-  const float pr = phi * inv, hr = half * inv;
-  const int a1 = (int)ceilf(pr - hr), b1 = (int)floorf(pr + hr);
-  const int lo1 = max(0, a1), hi1 = min(127, b1);
-  const int lo2 = max(0, a1 + 192), hi2 = min(127, b1 + 192);
-  const int len1 = valid ? max(0, hi1 - lo1 + 1) : 0, len2 = valid ? max(0, hi2 - lo2 + 1) : 0;
-  const int cnt = len1 + len2;
+  float pr = fast_atan2(b, a) * inv;                  // CCW angle from ray 0 in rays, (-96, 96]
+  pr = pr < -32.5f ? pr + 192.0f : pr;                // -> [-32.5, 159.5)
+  const float margin = (float)(0.25 * kRes);          // see lidar_window
+  const float x = fminf(rr * __builtin_amdgcn_rcpf(d), 1.0f);
+  // asin(x) <= x + (pi/2 - 1) x^3 (see lidar_window); boat inside: all rays
+  const float hr = (fmaf((float)(kPi / 2 - 1) * x, x * x, x) + margin) * inv;
+  const bool wide = (d <= rr * 1.001f) | (hr >= 32.5f);
+  const int lo = wide ? 0 : max(0, (int)ceilf(pr - hr));
+  const int hi = wide ? 127 : min(127, (int)floorf(pr + hr));
+  const int cnt = valid ? max(0, hi - lo + 1) : 0;
   const int incl = wave_incl_scan(cnt);
   const int off = wave_excl_of(incl);
   const int W = __builtin_amdgcn_readlane(incl, 63);
-  // Segment marks.  Window w (0, 1) of obstacle lane l is a run of pairs starting at o_w (off, then
-  // off + len1) that maps pair q to ray q + (lo_w - o_w).  Its mark, written at o_w, is
-  // (2 l + w + 1) << 16 | (lo_w - o_w + 32768): the segment id in the high bits keeps the max-scan in
-  // segment order and the ray offset rides in the low bits, so a pair finds its owner obstacle and
-  // its ray from one max-scan, with no per-pair gather of the owner's window.
-  const int o2 = off + len1;
-  const int m1 = ((2 * l + 1) << 16) | (lo1 - off + 32768);
-  const int m2 = ((2 * l + 2) << 16) | (lo2 - o2 + 32768);
+  // Segment marks: obstacle lane l's run of pairs starts at off and maps pair q to ray
+  // q + (lo - off).  Its mark, written at off, is (l + 1) << 16 | (lo - off + 32768): the owner in
+  // the high bits keeps the max-scan in run order and the ray offset rides in the low bits, so a
+  // pair finds its owner and its ray from one max-scan, with no per-pair gather of the owner's window.
+  const int mk0 = ((l + 1) << 16) | (lo - off + 32768);
   rec[l] = make_float4(a, b, rr * rr, __uint_as_float(ord_key(key)));
   int carry = 0;
   for (int base = 0; base < W; base += kWave) {       // wave-uniform pass count
     L.mark[l] = 0;
-    if (len1 > 0 && off >= base && off < base + kWave) L.mark[off - base] = m1;
-    if (len2 > 0 && o2 >= base && o2 < base + kWave) L.mark[o2 - base] = m2;
+    if (cnt > 0 && off >= base && off < base + kWave) L.mark[off - base] = mk0;
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");   // marks and records visible
     __builtin_amdgcn_wave_barrier();
     const int mk = max(wave_incl_max(L.mark[l]), carry);
     carry = __builtin_amdgcn_readlane(mk, 63);
     const int q = base + l;
-    const int jj = max(((mk >> 16) - 1) >> 1, 0);     // owner obstacle lane
+    const int jj = max((mk >> 16) - 1, 0);            // owner obstacle lane
     const int i = min(max(q + (mk & 0xffff) - 32768, 0), 127);
     const float4 o = rec[jj];                         // owner's (a, b, r^2, key bits)
     const float2 cs = L.rayoff[i];
@@ -963,8 +962,7 @@ __device__ __forceinline__ void lidar_window2(float dx, float dy, float key, flo
     const float perp = fmaf(o.x, cs.y, -(o.y * cs.x));
     const float delta = fmaf(-perp, perp, o.z);
     const float dist = proj - l_sqrt(delta);
-    bool hit = (q < W) & (proj >= 0.0f) & (delta >= 0.0f);
-    if (RANGE_CHECK) hit = hit && dist < (float)kSensorMax;   // :458
+    const bool hit = (q < W) & (proj >= 0.0f) & (delta >= 0.0f) & (!far | (dist < (float)kSensorMax));  // :458
     if (hit)                                          // slots: env A's rays, then env B's
       atomicMin(&L.slot[(jj >= 32 ? 128 : 0) + i], ((unsigned long long)__float_as_uint(o.w) << 32) | __float_as_uint(dist));
   }
@@ -999,9 +997,7 @@ __device__ __forceinline__ void lidar_wave2(float* rows, int os, int nl, float p
   A.term = (unsigned)tb != 0; B.term = (tb >> 32) != 0;
   A.far = B.far = false;
   const bool far = ballot(valid & (d >= (float)(0.99 * kSensorMax))) != 0;
-  const WinLds W{slot, mark, rayoff};
-  if (!far) lidar_window2<false>(dx, dy, key, d, rr, valid, c0r, s0r, reinterpret_cast<float4*>(rows), W, A, B);
-  else lidar_window2<true>(dx, dy, key, d, rr, valid, c0r, s0r, reinterpret_cast<float4*>(rows), W, A, B);
+  lidar_window2(dx, dy, key, d, rr, valid, far, c0r, s0r, reinterpret_cast<float4*>(rows), WinLds{slot, mark, rayoff}, A, B);
 }
 
 template <typename R, int LID, typename Row>
@@ -1455,7 +1451,7 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const int l = lane_id();
-  const int os = S.ostride, rowb = row_bytes<float>(S.cap);
+  constexpr int os = 32, rowb = row_bytes<float>(32);  // cap in [29, 32]: plane stride 32, 384-B rows
   const int eb = blockIdx.x * kQE;                     // this block's envs: eb .. eb + nbe - 1
   const int nbe = min(kQE, S.N - eb);
   const int np = (nbe + 1) >> 1;                       // and pairs 0 .. np - 1 (block-local)
@@ -1474,7 +1470,17 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
   USV_STAMP_W(0);
   USV_STAMP_ID();
   int cur = wave;
-  if (cur < np) dma_copy1(S.orow(eb + 2 * cur), rowbuf0, min(2, nbe - 2 * cur) * rowb);
+  // first (static) pairs: pair w's rows into wave w's buffer 0.  With the fused dynamics, waves 2 and 3
+  // also issue those of waves 0 and 1, whose state loads would otherwise queue behind their own DMA
+  // (a wave's loads return in issue order); the barrier below publishes them.
+  constexpr int kDynWaves = FUSED ? kQE / kWave : 0;
+  if (wave >= kDynWaves && cur < np) dma_copy1(S.orow(eb + 2 * cur), rowbuf0, min(2, nbe - 2 * cur) * rowb);
+  if (FUSED && wave >= kDynWaves && wave < 2 * kDynWaves) {
+    const int w = wave - kDynWaves;
+    if (w < np)
+      dma_copy1(S.orow(eb + 2 * w), lds + wave_tab_bytes<float>() + w * q_slice_bytes() + 256 * 8 + 64 * 4,
+                min(2, nbe - 2 * w) * rowb);
+  }
   if constexpr (FUSED) {
     // dynamics, one lane per env.  Lanes past the end repeat the wave's last env (same wave:
     // every lane loads the state before any lane stores it); a wave with no env of its own must
