@@ -112,16 +112,63 @@ def _cpu_worker(args):
     return n, time.perf_counter() - t0
 
 
-def cpu_baseline(env_id, seconds, procs):
+def host_cores():
+    """Cores this process may use: the affinity set, capped by a cgroup CPU quota when one is set
+    and by the host's declared CPU share (OMP_NUM_THREADS, which the GPU pool sets to the box's
+    share of the node: its affinity mask lists every CPU of the machine)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]       # cgroup v2: "max 100000"
+        if q != "max":
+            quota = float(q) / float(p)
+    except (OSError, ValueError):
+        try:                                                            # cgroup v1
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            quota = q / p if q > 0 else None
+        except (OSError, ValueError):
+            quota = None
+    cores = aff if quota is None else max(1, min(aff, int(quota)))
+    share = os.environ.get("OMP_NUM_THREADS", "")
+    if share.isdigit() and int(share) > 0:
+        cores = min(cores, int(share))
+    return cores, aff, quota
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(env_id, seconds, procs, affinity=None, quota=None):
     ctx = mp.get_context("spawn")
     with ctx.Pool(procs) as pool:
         res = pool.map(_cpu_worker, [(env_id, seconds, 1000 + i) for i in range(procs)])
     steps = sum(r[0] for r in res)
     rate = sum(r[0] / r[1] for r in res)
-    return {"value": round(rate, 1), "unit": "env-steps/s", "cores": procs, "kind": "port",
-            "sample": f"{procs} single-threaded processes x 1 env x ~{seconds:.0f}s of random-action "
-                      f"{env_id} steps with TimeLimit+autoreset ({steps} env-steps total); "
-                      "oracle/usv_oracle.py per-env float64 NumPy restatement of the reference step"}
+    out = {"value": round(rate, 1), "unit": "env-steps/s", "cores": procs, "kind": "port",
+           "cpu_model": cpu_model(), "affinity_cpus": affinity, "cgroup_quota_cpus": quota,
+           "declared_share": os.environ.get("OMP_NUM_THREADS"),
+           "sample": f"{procs} single-threaded processes (one per usable host core) x 1 env x ~{seconds:.0f}s "
+                     f"of random-action {env_id} steps with TimeLimit+autoreset ({steps} env-steps total); "
+                     "oracle/usv_oracle.py per-env float64 NumPy restatement of the reference step"}
+    # per-core speed of this restatement relative to the reference itself, measured in the build
+    # container (tools/calibrate_cpu.py; the reference does not exist on the GPU box)
+    cal_p = os.path.join(ROOT, "profiles", "cpu_calibration.json")
+    if os.path.exists(cal_p):
+        cal = json.load(open(cal_p)).get(env_id)
+        if cal:
+            ratio = cal["ratio_oracle_over_reference"]
+            out["calibration"] = {"oracle_over_reference_per_core": ratio,
+                                  "reference_equivalent_value": round(rate / ratio, 1),
+                                  "source": "profiles/cpu_calibration.json (tools/calibrate_cpu.py)"}
+    return out
 
 
 # --------------------------------------------------------------------------- main
@@ -136,7 +183,7 @@ def main():
     ap.add_argument("--lidar", default="window", choices=["brute", "window"])
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--cpu-procs", type=int, default=0, help="0 = min(16, available cores)")
+    ap.add_argument("--cpu-procs", type=int, default=0, help="0 = every usable host core")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--event-every", type=int, default=16, help="launches per HIP-event-timed group")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_summary.json"))
@@ -243,8 +290,8 @@ def main():
             out["config"].pop("lidar")
             out["config"].pop("mean_obstacles")
         if not args.no_cpu_baseline and world == 1:        # the CPU leg runs at N = 1 only
-            procs = args.cpu_procs or min(16, len(os.sched_getaffinity(0)))
-            out["cpu_baseline"] = cpu_baseline(args.env_id, args.cpu_seconds, procs)
+            cores, aff, quota = host_cores()
+            out["cpu_baseline"] = cpu_baseline(args.env_id, args.cpu_seconds, args.cpu_procs or cores, aff, quota)
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)

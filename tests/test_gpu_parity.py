@@ -63,11 +63,15 @@ def test_golden_trajectory_replay(golden, fname, env_id, precision):
     alive = np.ones(n, bool)
     worst = {"hdr": 0.0, "rew": 0.0}
     flips, rays = 0, 0
-    # f32 trajectories accumulate rounding along the rollout; ASMC adds 20 substeps per step
+    # f32 trajectories accumulate rounding along the rollout (about 5x the measured worst case,
+    # r02: usv-simple header 1.4e-6 / reward 1.3e-5; usv-asmc-simple 5.2e-6 / 1.0e-4).  The ASMC
+    # reward error is two ulps of a ~50 m float32 position (ye_reward slope 1/0.075 per m) after
+    # 20 substeps per step: past SURVEY §8(c)'s single-step 1e-4, which test_single_step_parity_4096
+    # holds; DESIGN.md "Oracle and parity" records this trajectory bound.
     if precision == "f64":
         hdr_tol, sens_tol, rew_tol = 2e-6, 2e-6, 1e-8
     else:
-        hdr_tol, sens_tol, rew_tol = (5e-4, 1e-4, 5e-3) if env_id == "usv-simple" else (2e-2, 1e-3, 5e-2)
+        hdr_tol, sens_tol, rew_tol = (7e-6, 1e-4, 7e-5) if env_id == "usv-simple" else (3e-5, 1e-4, 5e-4)
     for t in range(T):
         a = torch.from_numpy(g["actions"][:, t]).cuda()
         obs, rew, term, trunc, _ = env.step(a)
@@ -150,9 +154,8 @@ def test_single_step_parity_4096(env_id, precision, scatter):
     the field so obstacles beyond the 99 m far threshold occur (lidar max-range test)."""
     n = 4096 if env_id == "usv-simple" else 2048
     atol, rtol, ratol = (F32_OBS_ATOL, F32_OBS_RTOL, F32_REW_ATOL) if precision == "f32" else (2e-6, 1e-6, 1e-9)
-    if env_id == "usv-asmc-simple" and precision == "f32":
-        # 20 ASMC substeps in fp32: r_d = (psi_d - psi_d_last)/0.01 amplifies psi rounding
-        atol, rtol, ratol = 5e-4, 1e-3, 5e-3
+    # usv-asmc-simple f32 (20 ASMC substeps) holds the same SURVEY §8(c) bounds: r02 measured
+    # header 1.7e-6, reward 6.5e-5
     for k, s in enumerate(_single_step_round(env_id, n, precision, scatter=scatter)):
         assert s["term_mis"] <= max(1, n // 2000) and s["trunc_mis"] <= max(1, n // 2000), s
         ok = s["flags_ok"]
@@ -434,7 +437,8 @@ def test_v0_golden_trajectory_replay(golden, precision):
     _v0_inject(env, o, np.ones(n, bool))
     alive = np.ones(n, bool)
     worst_o = worst_r = 0.0
-    tol_o, tol_r = (5e-6, 1e-6) if precision == "f64" else (2e-3, 2e-3)
+    # r02 measured: f64 obs 9.5e-7 (the reference's own float32 rounding), f32 obs 9.5e-7 / reward 1.2e-6
+    tol_o, tol_r = (5e-6, 1e-6) if precision == "f64" else (5e-6, 6e-6)
     steps = T if precision == "f64" else 600      # f32 state drifts along chaotic ASMC switches
     for t in range(steps):
         obs, rew, term, trunc, _ = env.step(torch.from_numpy(g["actions"][:, t:t + 1]).cuda())
@@ -535,7 +539,8 @@ def test_legacy_f64_golden_trajectory_replay(golden, env_id, family, fname, prec
     _legacy_inject(env, o)
     alive = np.ones(n, bool)
     worst_o = worst_r = 0.0
-    tol_o, tol_r = (1e-6, 1e-8) if precision == "f64" else (2e-3, 2e-3)
+    # r02 measured f32 (600 steps): obs <= 5.6e-6, reward <= 7.6e-6
+    tol_o, tol_r = (1e-6, 1e-8) if precision == "f64" else (3e-5, 4e-5)
     steps = T if precision == "f64" else 600
     for t in range(steps):
         obs, rew, term, trunc, _ = env.step(torch.from_numpy(g["actions"][:, t:t + 1]).cuda())

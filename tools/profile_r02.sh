@@ -1,0 +1,24 @@
+# Round profile of the headline step kernel: kernel-trace stats, FETCH_SIZE / WRITE_SIZE passes,
+# three SQ counter passes (one rocprofv3 --pmc run each, no tracing domains combined), then the
+# bench line with roofline.traffic from the PMC summary.  Usage: bash tools/profile_r02.sh TAG
+set -e
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+R=${1:-r02}
+ENVS=${ENVS:-65536}
+OUT=gpurun_out/prof_$R
+mkdir -p $OUT
+B="python3 bench.py --envs $ENVS --no-cpu-baseline"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o kt --output-format csv -- $B --steps 2000 --warmup 100 > $OUT/kt.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o fetch --output-format csv -- $B --steps 40 --warmup 10 > $OUT/fetch.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o write --output-format csv -- $B --steps 40 --warmup 10 > $OUT/write.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY -d $OUT/sq/p1 -o p1 --output-format csv -- $B --steps 30 --warmup 5 > $OUT/p1.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INST_CYCLES_VMEM GRBM_GUI_ACTIVE SQ_WAIT_INST_ANY -d $OUT/sq/p2 -o p2 --output-format csv -- $B --steps 30 --warmup 5 > $OUT/p2.log 2>&1
+timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_SMEM SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_SALU SQ_LDS_UNALIGNED_STALL SQ_IFETCH -d $OUT/sq/p3 -o p3 --output-format csv -- $B --steps 30 --warmup 5 > $OUT/p3.log 2>&1
+python3 tools/pmc_all.py $OUT/sq --envs $ENVS > $OUT/sq_counters.txt
+cat $OUT/sq_counters.txt
+python3 tools/pmc_summary.py --kt $OUT/kt --fetch $OUT/fetch --write $OUT/write --key usv-simple/$ENVS/f32/window --round $R --out $OUT/profiles
+cp profiles/pmc_summary.json $OUT/pmc_summary_prev.json 2>/dev/null || true
+# bench last, with the default CPU leg: it reads roofline.traffic from the PMC summary just written
+timeout -k 10 300 python bench.py --envs $ENVS --pmc $OUT/profiles/pmc_summary.json > $OUT/bench.json 2> $OUT/bench.err
+tail -1 $OUT/bench.json
