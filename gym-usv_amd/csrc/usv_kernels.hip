@@ -1393,7 +1393,10 @@ __global__ __launch_bounds__(kWave * WPB) void scan_kernel(State<R> S, IO<R> io)
 // before the sensors reach them).
 // Each wave's first pair is static (pair = wave); its rows and the next pair's are DMA'd while
 // the current pair is scanned (one DMA instruction per pair: two 384-B SoA rows).
-constexpr int kQW = 16, kQE = 128, kQRec = 16;
+#ifndef USV_QE
+#define USV_QE 128       // envs per block-queue block (diagnostic builds may change it)
+#endif
+constexpr int kQW = 16, kQE = USV_QE, kQRec = 16;
 __host__ __device__ constexpr size_t q_slice_bytes() { return 256 * 8 + 64 * 4 + 2 * 1024; }
 __host__ __device__ constexpr size_t lds_q_bytes() {
   return wave_tab_bytes<float>() + kQW * q_slice_bytes() + kQE * kQRec * 4 + 16;
@@ -1537,6 +1540,8 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
       const int e0 = eb + k0;
       const bool hasB = k0 + 1 < nbe;
       const int nxt = (int)__builtin_amdgcn_readlane(tk, 0);
+      if (S.prio == 1) set_prio(3 - (4 * min(nxt, np)) / (np + 1));   // tuning: block-progress ramp
+      else if (S.prio == 3) set_prio((blockIdx.x >= (gridDim.x >> 1)) && 2 * nxt < np ? 1 : 0);
       if (nxt < np) {                                   // wave-uniform
         if (l == 0) tk = atomicAdd(qctr, 1u);
         dma_copy1(S.orow(eb + 2 * nxt), nbuf, min(2, nbe - 2 * nxt) * rowb);
@@ -1548,6 +1553,23 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
       const float4 meta = *reinterpret_cast<const float4*>(rk + 4);
       const int nt = __float_as_int(meta.y);
       Scan<float> sa, sb;
+#if defined(USV_ABL_VALU) || defined(USV_ABL_SALU)   // diagnostic only: N extra independent VALU / SALU ops per pair
+      {
+        float d0 = pose.x, d1 = pose.y, d2 = pose.z, d3 = pose.w;
+        int s0 = cur, s1 = cur + 1, s2 = cur + 2, s3 = cur + 3;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+#ifdef USV_ABL_VALU
+          asm volatile("v_add_f32 %0, %0, %1\n\tv_add_f32 %2, %2, %1\n\tv_add_f32 %3, %3, %1\n\tv_add_f32 %4, %4, %1"
+                       : "+v"(d0), "+v"(d1) : "v"(d2), "v"(d3), "v"(d1));
+#else
+          asm volatile("s_add_u32 %0, %0, %1\n\ts_add_u32 %2, %2, %1\n\ts_add_u32 %3, %3, %1\n\ts_add_u32 %4, %4, %1"
+                       : "+s"(s0), "+s"(s1) : "s"(s2), "s"(s3), "s"(s1));
+#endif
+        }
+        if (d0 == 12345.0f && s0 == 77) io.rew[0] = d1 + (float)s1;   // keep the chains live
+      }
+#endif
 #ifdef USV_ABL_NOLIDAR   // diagnostic ablation only: readings from the row and pose, no scan
       sa.rd0 = cbuf[l & 31] + pose.x; sa.rd1 = pose.y + pose.z; sa.term = sa.far = false;
       sb = sa;
@@ -2539,9 +2561,9 @@ int usv_create(const usv_config* cfg, int32_t device, void** out) {
   if (cfg->mode == USV_MODE_ASMC_SIMPLE) {
     // ASMC's 20 substeps want full-width dynamics: a separate dyn_kernel, then the block queue
     // (45.7 us vs 46.7 for the split wave scan at 65 536 envs)
-    if (queue) { h->kind = 4; h->epb = 128; } else { h->kind = 2; h->epb = 16; }
+    if (queue) { h->kind = 4; h->epb = kQE; } else { h->kind = 2; h->epb = 16; }
   } else if (queue) {
-    h->kind = 5; h->epb = 128;          // block-queue step, 16-wave blocks
+    h->kind = 5; h->epb = kQE;          // block-queue step, 16-wave blocks
   } else { h->kind = 1; h->epb = 64; }
   if (const char* v = std::getenv("USV_STEP_VARIANT")) {   // "epb,lid[,kind]" tuning override
     int epb = 0, lid = 0, kind = 0;
