@@ -161,6 +161,33 @@ struct Prof {
   __device__ void flush(int) {}
 };
 #endif
+// Diagnostic build only (-DUSV_DIAG_QPROF): per-wave shader-clock cycles (s_memtime; its SMEM
+// round trip also waits for the wave's LDS ops, so the marks perturb what they time) spent in each section of the block-queue step, read back with usv_diag_qprof().
+constexpr int kQProfSlots = 12;
+#ifdef USV_DIAG_QPROF
+__device__ unsigned g_qprof[16384 * kQProfSlots];
+__device__ __forceinline__ unsigned shader_cycles() { return (unsigned)__builtin_amdgcn_s_memtime(); }
+struct QProf {
+  unsigned acc[kQProfSlots];
+  unsigned t;
+  __device__ QProf() : t(shader_cycles()) { for (int i = 0; i < kQProfSlots; ++i) acc[i] = 0; }
+  __device__ __forceinline__ void mark(int i) { const unsigned n = shader_cycles(); acc[i] += n - t; t = n; }
+  __device__ __forceinline__ void count(int i, unsigned k = 1) { acc[i] += k; }
+  __device__ void flush() {
+    const unsigned gw = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
+    if ((threadIdx.x & 63) == 0 && gw < 16384)
+      for (int k = 0; k < kQProfSlots; ++k) g_qprof[gw * kQProfSlots + k] = acc[k];
+  }
+};
+#define QMARK(i) do { if (qp) qp->mark(i); } while (0)
+__device__ __forceinline__ void qprof_flush(QProf* qp) { qp->flush(); }
+#define QCOUNT(i, k) do { if (qp) qp->count(i, k); } while (0)
+#else
+struct QProf { __device__ void mark(int) {} __device__ void count(int, unsigned = 1) {} __device__ void flush() {} };
+#define QMARK(i) do {} while (0)
+#define QCOUNT(i, k) do {} while (0)
+__device__ __forceinline__ void qprof_flush(QProf*) {}
+#endif
 template <typename R> struct Vec2;
 template <> struct Vec2<float> { using T = float2; };
 template <> struct Vec2<double> { using T = double2; };
@@ -727,6 +754,7 @@ template <typename R> struct Scan { R rd0, rd1; bool term, far; };
 
 // |atan2(y, x)| error < 7e-4 rad = 0.02 ray (degree-5 minimax on [0,1] + octant folding), well inside
 // the quarter-ray window margin; only used to size the conservative ray windows, never for a reading.
+// atan2 to |err| <= 6.1e-4 rad (degree-5 odd minimax on [0, 1] plus octant folding)
 __device__ __forceinline__ float fast_atan2(float y, float x) {
   const float ax = fabsf(x), ay = fabsf(y);
   const float mx = fmaxf(fmaxf(ax, ay), 1e-30f), mn = fminf(ax, ay);
@@ -737,6 +765,8 @@ __device__ __forceinline__ float fast_atan2(float y, float x) {
   p = x < 0.0f ? 3.14159265f - p : p;
   return y < 0.0f ? -p : p;
 }
+
+constexpr double kWinMargin = 0.05;   // ray-window margin of the window lidar, in rays (lidar_window)
 
 __device__ __forceinline__ unsigned ord_key(float k) {   // float -> order-preserving uint
   const unsigned u = __float_as_uint(k);
@@ -840,9 +870,10 @@ __device__ __forceinline__ void lidar_window(float dx, float dy, float key, floa
   float a, b;
   to_ray0(dx, dy, c0r, s0r, a, b);
   const float phi = fast_atan2(b, a);                 // CCW angle from ray 0; ray i at i*res
-  // |err| of the window edges: fast_atan2 < 2e-5 rad, float rounding ~1e-6 rad; a ray
-  // 1e-5 rad outside the true extent already fails the exact test by ~r*d*1e-5 >> ulp
-  const float margin = (float)(0.25 * kRes);
+  // |err| of the window edges: fast_atan2 <= 6.1e-4 rad (0.019 ray), float rounding ~1e-6 rad; a
+  // ray 1e-5 rad outside the true extent already fails the exact test by ~r*d*1e-5 >> ulp.  The
+  // margin (0.05 ray = 1.6e-3 rad) covers both 2.6x over.
+  const float margin = (float)(kWinMargin * kRes);
   const bool inside = d <= rr * 1.001f;
   // asin(x) <= x + (pi/2 - 1) x^3 on [0, 1] (Taylor coefficients >= 0 summing to pi/2 at x = 1)
   const float x = fminf(rr * __builtin_amdgcn_rcpf(d), 1.0f);
@@ -921,14 +952,14 @@ __device__ __forceinline__ void lidar_window(float dx, float dy, float key, floa
 // (usv_asmc_ca_env.py:458) can matter; it is applied to every pair then.
 __device__ __forceinline__ void lidar_window2(float dx, float dy, float key, float d, float rr, bool valid, bool far,
                                               float c0r, float s0r, float4* rec, const WinLds& L,
-                                              Scan<float>& A, Scan<float>& B) {
+                                              Scan<float>& A, Scan<float>& B, QProf* qp = nullptr) {
   const int l = lane_id();
   float a, b;
   to_ray0(dx, dy, c0r, s0r, a, b);
   const float inv = (float)(1.0 / kRes);
   float pr = fast_atan2(b, a) * inv;                  // CCW angle from ray 0 in rays, (-96, 96]
   pr = pr < -32.5f ? pr + 192.0f : pr;                // -> [-32.5, 159.5)
-  const float margin = (float)(0.25 * kRes);          // see lidar_window
+  const float margin = (float)(kWinMargin * kRes);    // see lidar_window
   const float x = fminf(rr * __builtin_amdgcn_rcpf(d), 1.0f);
   // asin(x) <= x + (pi/2 - 1) x^3 (see lidar_window); boat inside: all rays
   const float hr = (fmaf((float)(kPi / 2 - 1) * x, x * x, x) + margin) * inv;
@@ -945,9 +976,12 @@ __device__ __forceinline__ void lidar_window2(float dx, float dy, float key, flo
   // pair finds its owner and its ray from one max-scan, with no per-pair gather of the owner's window.
   const int mk0 = ((l + 1) << 16) | (lo - off + 32768);
   rec[l] = make_float4(a, b, rr * rr, __uint_as_float(ord_key(key)));
+  // The marks are cleared once per call (below), not per pass: a mark left by an earlier pass of
+  // this call is <= that pass's carry, which the max-scan folds in anyway.
   int carry = 0;
+  QMARK(2);
   for (int base = 0; base < W; base += kWave) {       // wave-uniform pass count
-    L.mark[l] = 0;
+    QCOUNT(9, 1);
     if (cnt > 0 && off >= base && off < base + kWave) L.mark[off - base] = mk0;
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");   // marks and records visible
     __builtin_amdgcn_wave_barrier();
@@ -958,24 +992,32 @@ __device__ __forceinline__ void lidar_window2(float dx, float dy, float key, flo
     const int i = min(max(q + (mk & 0xffff) - 32768, 0), 127);
     const float4 o = rec[jj];                         // owner's (a, b, r^2, key bits)
     const float2 cs = L.rayoff[i];
+    // slot of (owner env, ray) and the key half of the payload, before the hit branch (the whole
+    // record is read by one ds_read_b128: the key is not re-read inside the branch)
+    unsigned long long* const sl = &L.slot[(jj >= 32 ? 128 : 0) + i];
+    const unsigned kb = __float_as_uint(o.w);
+    asm volatile("" :: "v"(kb));
     const float proj = fmaf(o.x, cs.x, o.y * cs.y);
     const float perp = fmaf(o.x, cs.y, -(o.y * cs.x));
     const float delta = fmaf(-perp, perp, o.z);
     const float dist = proj - l_sqrt(delta);
     const bool hit = (q < W) & (proj >= 0.0f) & (delta >= 0.0f) & (!far | (dist < (float)kSensorMax));  // :458
     if (hit)                                          // slots: env A's rays, then env B's
-      atomicMin(&L.slot[(jj >= 32 ? 128 : 0) + i], ((unsigned long long)__float_as_uint(o.w) << 32) | __float_as_uint(dist));
+      atomicMin(sl, ((unsigned long long)kb << 32) | __float_as_uint(dist));
   }
+  QMARK(3);
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");     // all lanes' ds_min_u64 landed
   __builtin_amdgcn_wave_barrier();
   const unsigned long long a0 = L.slot[l], a1s = L.slot[l + 64];
   const unsigned long long b0 = L.slot[128 + l], b1s = L.slot[192 + l];
   L.slot[l] = ~0ull; L.slot[l + 64] = ~0ull;          // re-arm for this wave's next pair
   L.slot[128 + l] = ~0ull; L.slot[192 + l] = ~0ull;
+  L.mark[l] = 0;
   A.rd0 = a0 != ~0ull ? __uint_as_float((unsigned)a0) : (float)kSensorMax;
   A.rd1 = a1s != ~0ull ? __uint_as_float((unsigned)a1s) : (float)kSensorMax;
   B.rd0 = b0 != ~0ull ? __uint_as_float((unsigned)b0) : (float)kSensorMax;
   B.rd1 = b1s != ~0ull ? __uint_as_float((unsigned)b1s) : (float)kSensorMax;
+  QMARK(4);
 }
 
 // rows: LDS buffer (>= 1 KiB, reused for the per-obstacle records) holding env A's obstacle row
@@ -983,7 +1025,7 @@ __device__ __forceinline__ void lidar_window2(float dx, float dy, float key, flo
 // (px, py), ray-0 direction (c0r, s0r) and obstacle count nl (0: no env in this half).
 __device__ __forceinline__ void lidar_wave2(float* rows, int os, int nl, float px, float py, float c0r,
                                             float s0r, const float2* rayoff, unsigned long long* slot,
-                                            int* mark, Scan<float>& A, Scan<float>& B) {
+                                            int* mark, Scan<float>& A, Scan<float>& B, QProf* qp = nullptr) {
   const int l = lane_id();
   const int jl = l & 31;
   const bool valid = jl < nl;
@@ -997,7 +1039,7 @@ __device__ __forceinline__ void lidar_wave2(float* rows, int os, int nl, float p
   A.term = (unsigned)tb != 0; B.term = (tb >> 32) != 0;
   A.far = B.far = false;
   const bool far = ballot(valid & (d >= (float)(0.99 * kSensorMax))) != 0;
-  lidar_window2(dx, dy, key, d, rr, valid, far, c0r, s0r, reinterpret_cast<float4*>(rows), WinLds{slot, mark, rayoff}, A, B);
+  lidar_window2(dx, dy, key, d, rr, valid, far, c0r, s0r, reinterpret_cast<float4*>(rows), WinLds{slot, mark, rayoff}, A, B, qp);
 }
 
 template <typename R, int LID, typename Row>
@@ -1121,6 +1163,7 @@ __device__ __forceinline__ void scan_prologue(const State<R>& S, const ScanLds<R
   if (ne > 0) dma_copy(S.orow(e0), L.row0, min(scan_step<R, LID>(cap), ne) * row_bytes<R>(cap));
 #pragma unroll
   for (int i = 0; i < 4; ++i) L.slot[i * 64 + lane_id()] = ~0ull;
+  L.mark[lane_id()] = 0;                              // lidar_window2 clears them after each call
 }
 
 // VALU issue is arbitrated by priority, then age (MI355X_MICROARCH.md, Two waves per SIMD): with
@@ -1398,20 +1441,29 @@ __global__ __launch_bounds__(kWave * WPB) void scan_kernel(State<R> S, IO<R> io)
 #endif
 constexpr int kQW = 16, kQE = USV_QE, kQRec = 16;
 __host__ __device__ constexpr size_t q_slice_bytes() { return 256 * 8 + 64 * 4 + 2 * 1024; }
-__host__ __device__ constexpr size_t lds_q_bytes() {
-  return wave_tab_bytes<float>() + kQW * q_slice_bytes() + kQE * kQRec * 4 + 16;
-}
-static_assert(2 * lds_q_bytes() <= 160 * 1024, "two blocks per CU");
 
 // One DMA instruction (<= 64 pieces of 16 B, i.e. <= 1 KiB): pieces c >= nchunk are not copied.
+// src is wave-uniform: SGPR base + a 32-bit lane offset (the saddr form), so no per-lane 64-bit
+// address is kept live across the pair loop.
 __device__ __forceinline__ void dma_copy1(const void* src, void* dst, int bytes) {
   const int c = lane_id();
   const unsigned d = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)dst);
+  const uint64_t a = (uint64_t)(uintptr_t)src;
+  // (readfirstlane returns int: widen through unsigned, or the low half would sign-extend)
+  const uint64_t sb = ((uint64_t)(unsigned)__builtin_amdgcn_readfirstlane((unsigned)(a >> 32)) << 32) |
+                      (uint64_t)(unsigned)__builtin_amdgcn_readfirstlane((unsigned)a);
   if (c < bytes / 16) {
     unsigned keep;
+#ifdef USV_DMA_VADDR      // (diagnostic: per-lane 64-bit address form)
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
                  "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep) : "v"(reinterpret_cast<const char*>(src) + 16 * (size_t)c), "s"(d) : "memory");
+    (void)sb;
+#else
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(16 * c), "s"(sb), "s"(d) : "memory");
+#endif
   }
 }
 
@@ -1449,6 +1501,11 @@ __device__ __forceinline__ void q_emit_done(const State<float>& S, const IO<floa
   }
 }
 
+__host__ __device__ constexpr size_t lds_q_bytes() {
+  return wave_tab_bytes<float>() + kQW * q_slice_bytes() + kQE * kQRec * 4 + 16;
+}
+static_assert(2 * lds_q_bytes() <= 160 * 1024, "two blocks per CU");
+
 template <int MODE, bool FUSED>
 __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<float>& io) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -1466,18 +1523,25 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
   float* const recs = reinterpret_cast<float*>(lds + wave_tab_bytes<float>() + kQW * q_slice_bytes());
   unsigned* const qctr = reinterpret_cast<unsigned*>(recs + kQE * kQRec);
   const float2* const rayoff = reinterpret_cast<const float2*>(lds);
+#ifdef USV_DIAG_QPROF
+  QProf qprof;
+  QProf* const qp = &qprof;
+#else
+  QProf* const qp = nullptr;
+#endif
   if (threadIdx.x == 0) *qctr = kQW;                   // pairs 0 .. kQW-1 are the static first ones
   if (wave == 0) dma_copy(S.ray_tab, lds, (int)wave_tab_bytes<float>());
 #pragma unroll
   for (int i = 0; i < 4; ++i) slot[i * 64 + l] = ~0ull;
+  mark[l] = 0;                                         // lidar_window2 clears them after each call
   USV_STAMP_W(0);
   USV_STAMP_ID();
-  int cur = wave;
+  int cur = wave < np ? wave : -1;
   // first (static) pairs: pair w's rows into wave w's buffer 0.  With the fused dynamics, waves 2 and 3
   // also issue those of waves 0 and 1, whose state loads would otherwise queue behind their own DMA
   // (a wave's loads return in issue order); the barrier below publishes them.
   constexpr int kDynWaves = FUSED ? kQE / kWave : 0;
-  if (wave >= kDynWaves && cur < np) dma_copy1(S.orow(eb + 2 * cur), rowbuf0, min(2, nbe - 2 * cur) * rowb);
+  if (wave >= kDynWaves && cur >= 0) dma_copy1(S.orow(eb + 2 * cur), rowbuf0, min(2, nbe - 2 * cur) * rowb);
   if (FUSED && wave >= kDynWaves && wave < 2 * kDynWaves) {
     const int w = wave - kDynWaves;
     if (w < np)
@@ -1512,12 +1576,14 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
   // rows, ray table and records landed
   USV_STAMP_W(1);
   vm_wait<0>();
+  QMARK(10);
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   USV_STAMP_W(2);
+  QMARK(0);
   unsigned tk = 0;
   if (l == 0) tk = atomicAdd(qctr, 1u);                 // LDS ticket of this wave's second pair
-  // same-step autoresets of a pair run outside the pair loop (the loop is left after a pair with
-  // a done env and re-entered): inside it their registers would spill the loop's to scratch
+  // same-step autoresets of a pair run outside the pair loop (the loop is left and re-entered):
+  // inside it their registers would spill the loop's to scratch
   int it = 0;
   const bool hb = l >= 32;
   // obs-header lanes (loop-invariant, packed in one register): lanes 0..14 store env A's header
@@ -1530,53 +1596,53 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
     const int hrec = hi == 0 ? 6 : (hi <= 9 ? hi + 5 : 15);
     hpk = hi | (hrec << 8) | ((hl >= kHdr) << 16) | ((hi == 1 || hi == 10 || hi >= 12) << 17);
   }
+  auto pair_hasb = [&](int p) { return 2 * p + 1 < nbe; };
+  // env record of pair c for this lane (lanes 0..31 env A, 32..63 env B; env A again when there is
+  // no B): pose, meta and the obs-header value this lane stores.  Read one pair ahead (after the
+  // current pair's scan), so the LDS latency overlaps the current pair's stores.
+  auto rec_of = [&](int c, float4& P, float4& M, float& H) {
+    const int c0 = 2 * c;
+    const bool cB = pair_hasb(c);
+    const float* const rk = recs + ((hb && cB) ? c0 + 1 : c0) * kQRec;
+    P = *reinterpret_cast<const float4*>(rk);
+    M = *reinterpret_cast<const float4*>(rk + 4);
+    H = recs[((((hpk >> 16) & 1) && cB) ? c0 + 1 : c0) * kQRec + ((hpk >> 8) & 31)];
+  };
   for (;;) {
     unsigned done = 0;
     int de0 = 0;
-    for (; cur < np; ++it) {
+    float4 pose = make_float4(0.f, 0.f, 0.f, 0.f), meta = pose;
+    float hv = 0.0f;
+    if (cur >= 0) rec_of(cur, pose, meta, hv);
+    while (cur >= 0) {
+      int nxt = (int)__builtin_amdgcn_readlane(tk, 0);
+      QCOUNT(8, 1);
       float* const cbuf = (it & 1) ? rowbuf1 : rowbuf0;
       float* const nbuf = (it & 1) ? rowbuf0 : rowbuf1;
       const int k0 = 2 * cur;
       const int e0 = eb + k0;
-      const bool hasB = k0 + 1 < nbe;
-      const int nxt = (int)__builtin_amdgcn_readlane(tk, 0);
-      if (S.prio == 1) set_prio(3 - (4 * min(nxt, np)) / (np + 1));   // tuning: block-progress ramp
-      else if (S.prio == 3) set_prio((blockIdx.x >= (gridDim.x >> 1)) && 2 * nxt < np ? 1 : 0);
-      if (nxt < np) {                                   // wave-uniform
+      const bool hasB = pair_hasb(cur);
+      if (nxt >= np) nxt = -1;
+      if (nxt >= 0) {                                  // wave-uniform
         if (l == 0) tk = atomicAdd(qctr, 1u);
-        dma_copy1(S.orow(eb + 2 * nxt), nbuf, min(2, nbe - 2 * nxt) * rowb);
+        dma_copy1(S.orow(eb + 2 * nxt), nbuf, (pair_hasb(nxt) ? 2 : 1) * rowb);
       }
       // this lane's env: lanes 0..31 env A, 32..63 env B (env A again when there is no B)
       const int kl = (hb && hasB) ? k0 + 1 : k0;
-      const float* const rk = recs + kl * kQRec;
-      const float4 pose = *reinterpret_cast<const float4*>(rk);
-      const float4 meta = *reinterpret_cast<const float4*>(rk + 4);
+      const int el = e0 + (kl - k0);
       const int nt = __float_as_int(meta.y);
       Scan<float> sa, sb;
-#if defined(USV_ABL_VALU) || defined(USV_ABL_SALU)   // diagnostic only: N extra independent VALU / SALU ops per pair
-      {
-        float d0 = pose.x, d1 = pose.y, d2 = pose.z, d3 = pose.w;
-        int s0 = cur, s1 = cur + 1, s2 = cur + 2, s3 = cur + 3;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-#ifdef USV_ABL_VALU
-          asm volatile("v_add_f32 %0, %0, %1\n\tv_add_f32 %2, %2, %1\n\tv_add_f32 %3, %3, %1\n\tv_add_f32 %4, %4, %1"
-                       : "+v"(d0), "+v"(d1) : "v"(d2), "v"(d3), "v"(d1));
-#else
-          asm volatile("s_add_u32 %0, %0, %1\n\ts_add_u32 %2, %2, %1\n\ts_add_u32 %3, %3, %1\n\ts_add_u32 %4, %4, %1"
-                       : "+s"(s0), "+s"(s1) : "s"(s2), "s"(s3), "s"(s1));
-#endif
-        }
-        if (d0 == 12345.0f && s0 == 77) io.rew[0] = d1 + (float)s1;   // keep the chains live
-      }
-#endif
 #ifdef USV_ABL_NOLIDAR   // diagnostic ablation only: readings from the row and pose, no scan
       sa.rd0 = cbuf[l & 31] + pose.x; sa.rd1 = pose.y + pose.z; sa.term = sa.far = false;
       sb = sa;
 #else
+      QMARK(1);
       lidar_wave2(cbuf, os, (hb && !hasB) ? 0 : (nt & 0xffff), pose.x, pose.y, pose.z, pose.w, rayoff, slot,
-                  mark, sa, sb);
+                  mark, sa, sb, qp);
 #endif
+      float4 pose_n = pose, meta_n = meta;
+      float hv_n = hv;
+      if (nxt >= 0) rec_of(nxt, pose_n, meta_n, hv_n);   // the next pair's record (wave-uniform)
       // env B's outputs (env A's again when there is none: identical stores to the same addresses
       // keep every memory instruction of the loop non-divergent and its count static)
       const int eB = hasB ? e0 + 1 : e0;
@@ -1594,15 +1660,14 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
       {                                                 // headers: lanes 0..14 env A, 15..29 env B
         const int hi = hpk & 31;
         const bool hB = ((hpk >> 16) & 1) && hasB;      // (no env B: env A's value again)
-        const float hv = recs[(hB ? k0 + 1 : k0) * kQRec + ((hpk >> 8) & 31)];
         const float hc = hi == 12 ? (float)(kMaxAccU / 10.0) : hi == 14 ? (float)(kMaxAccR / 10.0) : 0.0f;
         rowA[(hB ? kObsDim : 0) + hi] = ((hpk >> 17) & 1) ? hc : hv;
       }
 #endif
       const bool term_l = hb ? termB : sa.term;         // reward, terminated: lanes 0..31 env A,
       const bool coll_l = hb ? collB : collA;           // 32..63 env B
-      io.rew[eb + kl] = coll_l ? -20.0f + meta.x : meta.x;
-      io.term[eb + kl] = term_l;
+      io.rew[el] = coll_l ? -20.0f + meta.x : meta.x;
+      io.term[el] = term_l;
       const unsigned long long dm = ballot(term_l | ((nt >> 16) & 1));
       const bool doneA = (unsigned)dm != 0, doneB = hasB && (dm >> 32) != 0;
       if (doneA | doneB) {
@@ -1611,25 +1676,34 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
       }
       // the next pair's rows landed: at least seven stores (four sensor halves, the headers, the
       // rewards and the terminated flags) were issued after their DMA
+      QMARK(5);
 #ifdef USV_ABL_NOSTORE
       vm_wait<2>();
 #else
       vm_wait<7>();
 #endif
+      QMARK(6);
       cur = nxt;
+      pose = pose_n;
+      meta = meta_n;
+      hv = hv_n;
+      ++it;
       if (S.autoreset == USV_AUTORESET_SAME_STEP && (doneA | doneB)) {
         done = (doneA ? 1u : 0u) | (doneB ? 2u : 0u);
         de0 = e0;
-        ++it;
         break;
       }
     }
     if (!done) break;
+    QMARK(11);
     for (; done; done &= done - 1) {
       const int e = de0 + __builtin_ctz(done);
       reset_wave<float, MODE>(S, e, io.obs + (size_t)e * kObsDim);
     }
+    QMARK(7);
   }
+  QMARK(11);
+  qprof_flush(qp);
   USV_STAMP_W(3);
   USV_STAMP_W(6);
 }
@@ -2500,6 +2574,13 @@ int usv_abi_version(void) { return USV_ABI_VERSION; }
 int usv_diag_prof(void* host, size_t bytes) {
   HIP_TRY(hipDeviceSynchronize());
   HIP_TRY(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_prof), bytes < sizeof(g_prof) ? bytes : sizeof(g_prof)));
+  return USV_OK;
+}
+#endif
+#ifdef USV_DIAG_QPROF
+int usv_diag_qprof(void* host, size_t bytes) {
+  HIP_TRY(hipDeviceSynchronize());
+  HIP_TRY(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_qprof), bytes < sizeof(g_qprof) ? bytes : sizeof(g_qprof)));
   return USV_OK;
 }
 #endif

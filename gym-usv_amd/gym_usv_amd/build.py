@@ -15,6 +15,12 @@ INCLUDE = os.path.join(ROOT, "include")
 ARCH = os.environ.get("USV_OFFLOAD_ARCH", "gfx950")
 
 
+# The block-queue step takes its next pair's LDS ticket one pair ahead; the atomic optimizer would
+# rewrite that single-lane atomicAdd into a wave reduction whose result is consumed at once, exposing
+# the LDS atomic's latency every pair.
+DEVICE_FLAGS = ["-mllvm", "-amdgpu-atomic-optimizer-strategy=None"]
+
+
 def hipcc():
     for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", "hipcc"):
         if c and (os.path.isabs(c) and os.path.exists(c) or not os.path.isabs(c)):
@@ -40,7 +46,7 @@ def build_library(force=False, verbose=True):
         if all(os.path.getmtime(d) <= mt for d in deps()):
             return out
     cmd = [hipcc(), "-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-shared", "-Wall",
-           f"-I{INCLUDE}", "-o", out + ".tmp"] + sources()
+           *DEVICE_FLAGS, f"-I{INCLUDE}", "-o", out + ".tmp"] + sources()
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
