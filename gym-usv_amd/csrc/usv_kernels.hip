@@ -1131,9 +1131,17 @@ __device__ __forceinline__ void dma_copy(const void* src, void* dst, int bytes) 
 }
 // Wait until at most N vector-memory operations are outstanding (gfx9 vmcnt counts loads,
 // LDS-DMA and stores in issue order): everything older than the last N has completed.
+// Hand-counted vmcnt waits around the untracked inline-asm LDS-DMA.  The USV_SAFE_VMCNT build
+// (libusvhip_safe.so) turns every one into vmcnt(0); tests/test_gpu_r2.py checks it is bitwise
+// identical to the product build, so a miscounted wait (a DMA still in flight when its rows are
+// read) would show as a difference.
 template <int N> __device__ __forceinline__ void vm_wait() {
   static_assert(N >= 0 && N < 16, "vmcnt field");
+#ifdef USV_SAFE_VMCNT
+  __builtin_amdgcn_s_waitcnt(0x0F70);         // vmcnt(0)
+#else
   __builtin_amdgcn_s_waitcnt(0x0F70 | N);     // expcnt 7, lgkmcnt 15: no wait on those
+#endif
 }
 
 template <typename R> struct ScanLds {

@@ -83,32 +83,37 @@ SIGNATURES = [
     ("usv_set_state", ctypes.c_int, [_vp, _vp, _sz]),
 ]
 
-_LIB = None
+_LIBS = {}
 
 
-def load():
-    """Load (once) and return the HIP library; raise UsvLibError if it is unavailable."""
-    global _LIB
-    if _LIB is not None:
-        return _LIB
-    if not os.path.exists(LIB_PATH):
-        raise UsvLibError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+def load(path=None):
+    """Load (once per path) and return the HIP library; raise UsvLibError if it is unavailable.
+    ``path`` selects another build of the same C-ABI (e.g. libusvhip_safe.so); each path is its
+    own ctypes handle (RTLD_LOCAL), so two builds can be used side by side."""
+    path = path or LIB_PATH
+    if path in _LIBS:
+        return _LIBS[path]
+    if not os.path.exists(path):
+        raise UsvLibError(f"{path} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
     try:
-        lib = ctypes.CDLL(LIB_PATH)
+        lib = ctypes.CDLL(path)
     except OSError as e:  # pragma: no cover
-        raise UsvLibError(f"cannot load {LIB_PATH}: {e}") from e
+        raise UsvLibError(f"cannot load {path}: {e}") from e
     for name, res, args in SIGNATURES:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
     if lib.usv_abi_version() != ABI_VERSION:
         raise UsvLibError("libusvhip ABI version mismatch")
-    _LIB = lib
+    _LIBS[path] = lib
     return lib
 
 
-def check(rc):
+SAFE_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libusvhip_safe.so")
+
+
+def check(rc, lib=None):
     if rc != 0:
-        msg = load().usv_last_error().decode(errors="replace")
+        msg = (lib or load()).usv_last_error().decode(errors="replace")
         raise UsvLibError(f"libusvhip error {rc}: {msg}")
     return rc

@@ -39,14 +39,25 @@ def deps():
         [os.path.join(INCLUDE, "usv_hip.h")]
 
 
-def build_library(force=False, verbose=True):
-    out = os.path.join(PKG, "libusvhip.so")
-    if not force and os.path.exists(out):
-        mt = os.path.getmtime(out)
-        if all(os.path.getmtime(d) <= mt for d in deps()):
-            return out
-    cmd = [hipcc(), "-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-shared", "-Wall",
-           *DEVICE_FLAGS, f"-I{INCLUDE}", "-o", out + ".tmp"] + sources()
+# product library, and the debug build whose hand-counted vmcnt waits are all vmcnt(0)
+VARIANTS = {"product": ("libusvhip.so", []), "safe": ("libusvhip_safe.so", ["-DUSV_SAFE_VMCNT"])}
+
+
+def _stale(out):
+    return not os.path.exists(out) or any(os.path.getmtime(d) > os.path.getmtime(out) for d in deps())
+
+
+def _cmd(variant):
+    name, defs = VARIANTS[variant]
+    out = os.path.join(PKG, name)
+    return out, [hipcc(), "-O3", f"--offload-arch={ARCH}", "-std=c++17", "-fPIC", "-shared", "-Wall",
+                 *DEVICE_FLAGS, *defs, f"-I{INCLUDE}", "-o", out + ".tmp"] + sources()
+
+
+def build_library(force=False, verbose=True, variant="product"):
+    out, cmd = _cmd(variant)
+    if not force and not _stale(out):
+        return out
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)
@@ -54,5 +65,20 @@ def build_library(force=False, verbose=True):
     return out
 
 
+def build_all(force=False, verbose=True):
+    """Every variant, compiled concurrently (one hipcc process each)."""
+    jobs = []
+    for v in VARIANTS:
+        out, cmd = _cmd(v)
+        if force or _stale(out):
+            if verbose:
+                print(" ".join(cmd), flush=True)
+            jobs.append((out, subprocess.Popen(cmd)))
+    for out, p in jobs:
+        if p.wait() != 0:
+            raise subprocess.CalledProcessError(p.returncode, "hipcc " + out)
+        os.replace(out + ".tmp", out)
+
+
 if __name__ == "__main__":
-    build_library(force="--force" in sys.argv)
+    build_all(force="--force" in sys.argv)

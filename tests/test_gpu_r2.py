@@ -446,3 +446,38 @@ def test_two_process_sharding_bit_identical():
     total = sum(float(p["out"].double().sum()) for p in parts)
     assert abs(float(parts[0]["chk"]) - total) <= 1e-6 * abs(total)
     env.close()
+
+
+# --------------------------------------------------------------------------- vmcnt debug build
+@pytest.mark.parametrize("env_id,precision,variant", [
+    ("usv-simple", "f32", None),          # block-queue step (kind 5): LDS-DMA prefetch, vm_wait<7>
+    ("usv-asmc-simple", "f32", None),     # split block-queue step (kind 4)
+    ("usv-simple", "f32", "16,7,2"),      # split wave scan (kind 2): vm_wait<2|4>
+    ("usv-simple", "f64", None),          # fused wave kernel (kind 1)
+])
+def test_safe_vmcnt_build_bit_identical(env_id, precision, variant, monkeypatch):
+    """libusvhip_safe.so (USV_SAFE_VMCNT: every hand-counted vm_wait is vmcnt(0)) against the product
+    build over a rollout with resets: a miscounted wait in the product (a DMA'd obstacle row read
+    before it landed) would make them differ."""
+    from gym_usv_amd import _lib
+    if not os.path.exists(_lib.SAFE_LIB_PATH):
+        pytest.fail(f"{_lib.SAFE_LIB_PATH} not built (__graft_entry__.build() builds it)")
+    if variant:
+        monkeypatch.setenv("USV_STEP_VARIANT", variant)
+    n, T = 8192, 48
+    gen = torch.Generator(device="cuda").manual_seed(21)
+    acts = [torch.rand(n, 2, device="cuda", generator=gen) * torch.tensor([0.8, 2.0], device="cuda")
+            + torch.tensor([0.2, -1.0], device="cuda") for _ in range(T)]
+    outs = []
+    for path in (None, _lib.SAFE_LIB_PATH):
+        env = make(env_id, n, seed=13, precision=precision, max_episode_steps=20, lib_path=path)
+        env.reset(seed=13)
+        seq = []
+        for a in acts:
+            o, r, te, tr, info = env.step(a)
+            seq.append([x.clone() for x in (o, r, te, tr, info["final_obs"])])
+        env.close()
+        outs.append(seq)
+    for t, (x, y) in enumerate(zip(*outs)):
+        for u, v in zip(x, y):
+            assert torch.equal(u, v), f"safe-vmcnt build differs at step {t}"
