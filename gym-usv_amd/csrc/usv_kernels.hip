@@ -767,6 +767,10 @@ __device__ __forceinline__ float fast_atan2(float y, float x) {
 }
 
 constexpr double kWinMargin = 0.05;   // ray-window margin of the window lidar, in rays (lidar_window)
+// armed (no-hit) slot of lidar_window2: key bits all ones (above every ord_key of a finite or
+// infinite key, so any hit wins the ds_min_u64) and reading bits of the max range 100.0f
+constexpr unsigned long long kSlotArm = 0xFFFFFFFF42C80000ull;
+static_assert(kSensorMax == 100.0, "kSlotArm's reading half is 100.0f");
 
 __device__ __forceinline__ unsigned ord_key(float k) {   // float -> order-preserving uint
   const unsigned u = __float_as_uint(k);
@@ -860,6 +864,21 @@ __device__ __forceinline__ int wave_incl_max(int v) {
   return v;
 }
 
+// The same scan as fused DPP maxes in one asm block: a lane whose row is masked off by row_bcast keeps
+// its value (vdst = src1), so no zero-filled temporaries are needed.  s_nop 1 before each DPP read
+// of the VGPR the previous VALU wrote (gfx9 DPP hazard).
+__device__ __forceinline__ int wave_incl_max_asm(int v) {
+  asm volatile("s_nop 1\n\t"
+               "v_max_i32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\ts_nop 1\n\t"
+               "v_max_i32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\ts_nop 1\n\t"
+               "v_max_i32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\ts_nop 1\n\t"
+               "v_max_i32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\ts_nop 1\n\t"
+               "v_max_i32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\ts_nop 1\n\t"
+               "v_max_i32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf"
+               : "+v"(v));
+  return v;
+}
+
 template <bool RANGE_CHECK, typename Row>
 __device__ __forceinline__ void lidar_window(float dx, float dy, float key, float d, float rr, bool valid,
                                              float px, float py, float sp, float cp, const WinLds& L,
@@ -928,10 +947,10 @@ __device__ __forceinline__ void lidar_window(float dx, float dy, float key, floa
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");     // all lanes' ds_min_u64 landed
   __builtin_amdgcn_wave_barrier();
   const unsigned long long v0 = L.slot[l], v1 = L.slot[l + 64];
-  L.slot[l] = ~0ull;                                  // re-arm for this wave's next env
-  L.slot[l + 64] = ~0ull;
-  out.rd0 = v0 != ~0ull ? __uint_as_float((unsigned)v0) : (float)kSensorMax;
-  out.rd1 = v1 != ~0ull ? __uint_as_float((unsigned)v1) : (float)kSensorMax;
+  L.slot[l] = kSlotArm;                               // re-arm for this wave's next env
+  L.slot[l + 64] = kSlotArm;
+  out.rd0 = __uint_as_float((unsigned)v0);           // no hit: the armed payload, max range
+  out.rd1 = __uint_as_float((unsigned)v1);
 }
 
 // Two envs per wave (f32 window path, <= 32 obstacles each): lanes 0..31 hold env A's
@@ -970,11 +989,12 @@ __device__ __forceinline__ void lidar_window2(float dx, float dy, float key, flo
   const int incl = wave_incl_scan(cnt);
   const int off = wave_excl_of(incl);
   const int W = __builtin_amdgcn_readlane(incl, 63);
-  // Segment marks: obstacle lane l's run of pairs starts at off and maps pair q to ray
-  // q + (lo - off).  Its mark, written at off, is (l + 1) << 16 | (lo - off + 32768): the owner in
-  // the high bits keeps the max-scan in run order and the ray offset rides in the low bits, so a
-  // pair finds its owner and its ray from one max-scan, with no per-pair gather of the owner's window.
-  const int mk0 = ((l + 1) << 16) | (lo - off + 32768);
+  // Segment marks: obstacle lane l's run of pairs starts at off and maps pair q to slot
+  // q + (lo - off) + 128 [env B], i.e. ray (slot & 127).  Its mark, written at off, is
+  // (l + 1) << 16 | (lo - off + 128 [env B] + 32768): the owner in the high bits keeps the max-scan in
+  // run order and the slot offset rides in the low bits (in [24704, 33023]), so a pair finds its
+  // owner, its ray and its slot from one max-scan, with no per-pair gather of the owner's window.
+  const int mk0 = ((l + 1) << 16) | (lo - off + (l >= 32 ? 128 : 0) + 32768);
   rec[l] = make_float4(a, b, rr * rr, __uint_as_float(ord_key(key)));
   // The marks are cleared once per call (below), not per pass: a mark left by an earlier pass of
   // this call is <= that pass's carry, which the max-scan folds in anyway.
@@ -985,16 +1005,17 @@ __device__ __forceinline__ void lidar_window2(float dx, float dy, float key, flo
     if (cnt > 0 && off >= base && off < base + kWave) L.mark[off - base] = mk0;
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");   // marks and records visible
     __builtin_amdgcn_wave_barrier();
-    const int mk = max(wave_incl_max(L.mark[l]), carry);
+    const int mk = max(wave_incl_max_asm(L.mark[l]), carry);
     carry = __builtin_amdgcn_readlane(mk, 63);
     const int q = base + l;
     const int jj = max((mk >> 16) - 1, 0);            // owner obstacle lane
-    const int i = min(max(q + (mk & 0xffff) - 32768, 0), 127);
+    // slot of (owner env, ray): exact for q < W; other lanes (no hit) read some ray's offsets
+    const int si = q + (mk & 0xffff) - 32768;
     const float4 o = rec[jj];                         // owner's (a, b, r^2, key bits)
-    const float2 cs = L.rayoff[i];
-    // slot of (owner env, ray) and the key half of the payload, before the hit branch (the whole
-    // record is read by one ds_read_b128: the key is not re-read inside the branch)
-    unsigned long long* const sl = &L.slot[(jj >= 32 ? 128 : 0) + i];
+    const float2 cs = L.rayoff[si & 127];
+    // the key half of the payload before the hit branch (the whole record is read by one
+    // ds_read_b128: the key is not re-read inside the branch)
+    unsigned long long* const sl = &L.slot[si & 255];
     const unsigned kb = __float_as_uint(o.w);
     asm volatile("" :: "v"(kb));
     const float proj = fmaf(o.x, cs.x, o.y * cs.y);
@@ -1010,13 +1031,13 @@ __device__ __forceinline__ void lidar_window2(float dx, float dy, float key, flo
   __builtin_amdgcn_wave_barrier();
   const unsigned long long a0 = L.slot[l], a1s = L.slot[l + 64];
   const unsigned long long b0 = L.slot[128 + l], b1s = L.slot[192 + l];
-  L.slot[l] = ~0ull; L.slot[l + 64] = ~0ull;          // re-arm for this wave's next pair
-  L.slot[128 + l] = ~0ull; L.slot[192 + l] = ~0ull;
+  L.slot[l] = kSlotArm; L.slot[l + 64] = kSlotArm;    // re-arm for this wave's next pair
+  L.slot[128 + l] = kSlotArm; L.slot[192 + l] = kSlotArm;
   L.mark[l] = 0;
-  A.rd0 = a0 != ~0ull ? __uint_as_float((unsigned)a0) : (float)kSensorMax;
-  A.rd1 = a1s != ~0ull ? __uint_as_float((unsigned)a1s) : (float)kSensorMax;
-  B.rd0 = b0 != ~0ull ? __uint_as_float((unsigned)b0) : (float)kSensorMax;
-  B.rd1 = b1s != ~0ull ? __uint_as_float((unsigned)b1s) : (float)kSensorMax;
+  A.rd0 = __uint_as_float((unsigned)a0);              // no hit: the armed payload, max range
+  A.rd1 = __uint_as_float((unsigned)a1s);
+  B.rd0 = __uint_as_float((unsigned)b0);
+  B.rd1 = __uint_as_float((unsigned)b1s);
   QMARK(4);
 }
 
@@ -1030,8 +1051,9 @@ __device__ __forceinline__ void lidar_wave2(float* rows, int os, int nl, float p
   const int jl = l & 31;
   const bool valid = jl < nl;
   const float* rb = rows + (l >= 32 ? 3 * os : 0);
-  float ox = 0.0f, oy = 0.0f, rr = 0.0f;
-  if (valid) { ox = rb[jl]; oy = rb[os + jl]; rr = rb[2 * os + jl]; }
+  // read unconditionally: lanes past their env's obstacles (or of an absent env B) get slot padding
+  // or stale LDS, and every use below is masked by `valid`
+  const float ox = rb[jl], oy = rb[os + jl], rr = rb[2 * os + jl];
   const float dx = ox - px, dy = oy - py;
   const float d = l_sqrt(m_fma(dx, dx, dy * dy));
   const float key = valid ? d - rr : big<float>();                              // simple_env.py:205-206
@@ -1082,7 +1104,7 @@ __device__ __forceinline__ void lds_prologue(const State<R>& S, char* lds, int t
   auto* rayoff = reinterpret_cast<typename Vec2<R>::T*>(lds);
   auto* slots = reinterpret_cast<unsigned long long*>(lds + lds_rayoff_bytes<R>());
   if (tid < kSensors) rayoff[tid] = typename Vec2<R>::T{S.ray_tab[2 * tid], S.ray_tab[2 * tid + 1]};
-  for (int i = tid; i < kWaves * 128; i += kBlock) slots[i] = ~0ull;
+  for (int i = tid; i < kWaves * 128; i += kBlock) slots[i] = kSlotArm;
 }
 
 // --------------------------------------------------------------------------- wave-per-env scan
@@ -1170,7 +1192,7 @@ __device__ __forceinline__ void scan_prologue(const State<R>& S, const ScanLds<R
   if (wave == 0) dma_copy(S.ray_tab, L.rayoff, (int)wave_tab_bytes<R>());
   if (ne > 0) dma_copy(S.orow(e0), L.row0, min(scan_step<R, LID>(cap), ne) * row_bytes<R>(cap));
 #pragma unroll
-  for (int i = 0; i < 4; ++i) L.slot[i * 64 + lane_id()] = ~0ull;
+  for (int i = 0; i < 4; ++i) L.slot[i * 64 + lane_id()] = kSlotArm;
   L.mark[lane_id()] = 0;                              // lidar_window2 clears them after each call
 }
 
@@ -1540,7 +1562,7 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
   if (threadIdx.x == 0) *qctr = kQW;                   // pairs 0 .. kQW-1 are the static first ones
   if (wave == 0) dma_copy(S.ray_tab, lds, (int)wave_tab_bytes<float>());
 #pragma unroll
-  for (int i = 0; i < 4; ++i) slot[i * 64 + l] = ~0ull;
+  for (int i = 0; i < 4; ++i) slot[i * 64 + l] = kSlotArm;
   mark[l] = 0;                                         // lidar_window2 clears them after each call
   USV_STAMP_W(0);
   USV_STAMP_ID();
