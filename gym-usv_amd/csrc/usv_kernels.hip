@@ -1058,7 +1058,7 @@ __device__ __forceinline__ void lidar_wave2(float* rows, int os, int nl, float p
   const float d = l_sqrt(m_fma(dx, dx, dy * dy));
   const float key = valid ? d - rr : big<float>();                              // simple_env.py:205-206
   const unsigned long long tb = ballot(valid & (key < (float)kTermDist));       // :334
-  A.term = (unsigned)tb != 0; B.term = (tb >> 32) != 0;
+  A.term = (unsigned)tb != 0u; B.term = (unsigned)(tb >> 32) != 0u;
   A.far = B.far = false;
   const bool far = ballot(valid & (d >= (float)(0.99 * kSensorMax))) != 0;
   lidar_window2(dx, dy, key, d, rr, valid, far, c0r, s0r, reinterpret_cast<float4*>(rows), WinLds{slot, mark, rayoff}, A, B, qp);
@@ -1675,13 +1675,15 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
       if (nxt >= 0) rec_of(nxt, pose_n, meta_n, hv_n);   // the next pair's record (wave-uniform)
       // env B's outputs (env A's again when there is none: identical stores to the same addresses
       // keep every memory instruction of the loop non-divergent and its count static)
-      const int eB = hasB ? e0 + 1 : e0;
       const float sB0 = hasB ? sb.rd0 : sa.rd0, sB1 = hasB ? sb.rd1 : sa.rd1;
-      const bool collA = ballot((sa.rd0 < (float)kCollDist) | (sa.rd1 < (float)kCollDist)) != 0;   // :153-156
-      const bool collB = hasB ? ballot((sb.rd0 < (float)kCollDist) | (sb.rd1 < (float)kCollDist)) != 0 : collA;
+      // collision (:153-156): two compares and ballots per env (a fminf of the two readings would
+      // canonicalise both first)
+      const float kc = (float)kCollDist;
+      const bool collA = (ballot(sa.rd0 < kc) | ballot(sa.rd1 < kc)) != 0;
+      const bool collB = hasB ? (ballot(sb.rd0 < kc) | ballot(sb.rd1 < kc)) != 0 : collA;
       const bool termB = hasB ? sb.term : sa.term;
       float* const rowA = io.obs + (size_t)e0 * kObsDim;
-      float* const rowB = io.obs + (size_t)eB * kObsDim;
+      float* const rowB = rowA + (hasB ? kObsDim : 0);
 #ifndef USV_ABL_NOSTORE   // (diagnostic ablation: obs rows not written)
       rowA[kHdr + l] = l_norm(sa.rd0);                  // sensors (:82-83)
       rowA[kHdr + 64 + l] = l_norm(sa.rd1);
@@ -1699,7 +1701,7 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
       io.rew[el] = coll_l ? -20.0f + meta.x : meta.x;
       io.term[el] = term_l;
       const unsigned long long dm = ballot(term_l | ((nt >> 16) & 1));
-      const bool doneA = (unsigned)dm != 0, doneB = hasB && (dm >> 32) != 0;
+      const bool doneA = (unsigned)dm != 0u, doneB = hasB && (unsigned)(dm >> 32) != 0u;
       if (doneA | doneB) {
         if (doneA) q_emit_done(S, io, e0, sa, recs + k0 * kQRec);
         if (doneB) q_emit_done(S, io, e0 + 1, sb, recs + (k0 + 1) * kQRec);
