@@ -101,6 +101,29 @@ __device__ __forceinline__ void fx_sincos(float x, float* s, float* c) {
 }
 __device__ __forceinline__ void fx_sincos(double x, double* s, double* c) { sincos(x, s, c); }
 __device__ __forceinline__ float  fx_exp(float x)  { return __expf(x); }
+// atan2 for the f32 step's angle to target: octant reduction with an IEEE quotient and a degree-15
+// odd minimax polynomial (|err| <= 1.4e-7 rad on [0, 1] evaluated in float, ~1 ulp of pi after the
+// octant fold): ~20 VALU instead of libm's branchy atan2f on the phase-1 critical path.  The f64
+// build keeps libm.
+__device__ __forceinline__ float fx_atan2(float y, float x) {
+  const float ax = fabsf(x), ay = fabsf(y);
+  const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
+  const float t = mx > 0.0f ? mn / mx : 0.0f;
+  const float s = t * t;
+  float p = -0.004054558929055929f;
+  p = fmaf(p, s, 0.021862929686903954f);
+  p = fmaf(p, s, -0.055912286043167114f);
+  p = fmaf(p, s, 0.09642194956541061f);
+  p = fmaf(p, s, -0.1390862911939621f);
+  p = fmaf(p, s, 0.19946566224098206f);
+  p = fmaf(p, s, -0.33329859375953674f);
+  p = fmaf(p, s, 0.9999993443489075f);
+  p = p * t;
+  p = ay > ax ? 1.57079637f - p : p;
+  p = x < 0.0f ? 3.14159274f - p : p;
+  return copysignf(p, y);
+}
+__device__ __forceinline__ double fx_atan2(double y, double x) { return atan2(y, x); }
 __device__ __forceinline__ double fx_exp(double x) { return exp(x); }
 // x / c for a compile-time constant c: a multiply by the rounded reciprocal in f32 (<= 1 ulp
 // apart from the IEEE quotient), the IEEE division in f64

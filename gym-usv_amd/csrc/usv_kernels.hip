@@ -629,7 +629,7 @@ __device__ void env_dynamics(const State<R>& S, int e, float a_u, float a_r, flo
   const R sak = dy * inv_len, cak = dx * inv_len;
   const R ye = -(x - x0) * sak + (y - y0) * cak;
   // _get_angle_to_target (:67-69), distance (:74)
-  const R angle = wrap_angle(m_atan2(ty - y, tx - x) - psi);
+  const R angle = wrap_angle(fx_atan2(ty - y, tx - x) - psi);
   const R ddx = x - tx, ddy = y - ty;
   const R dist = m_sqrt(ddx * ddx + ddy * ddy);
   const int el = el0 + 1;
@@ -1057,10 +1057,13 @@ __device__ __forceinline__ void lidar_wave2(float* rows, int os, int nl, float p
   const float dx = ox - px, dy = oy - py;
   const float d = l_sqrt(m_fma(dx, dx, dy * dy));
   const float key = valid ? d - rr : big<float>();                              // simple_env.py:205-206
-  const unsigned long long tb = ballot(valid & (key < (float)kTermDist));       // :334
+  // ballots of plain compares ANDed on the SALU (a ballot of an ANDed condition makes the compiler
+  // materialise it per lane first)
+  const unsigned long long vm = ballot(valid);
+  const unsigned long long tb = vm & ballot(key < (float)kTermDist);            // :334
   A.term = (unsigned)tb != 0u; B.term = (unsigned)(tb >> 32) != 0u;
   A.far = B.far = false;
-  const bool far = ballot(valid & (d >= (float)(0.99 * kSensorMax))) != 0;
+  const bool far = (vm & ballot(d >= (float)(0.99 * kSensorMax))) != 0;
   lidar_window2(dx, dy, key, d, rr, valid, far, c0r, s0r, reinterpret_cast<float4*>(rows), WinLds{slot, mark, rayoff}, A, B, qp);
 }
 
