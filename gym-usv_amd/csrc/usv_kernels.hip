@@ -1534,12 +1534,18 @@ __device__ __forceinline__ void q_emit_done(const State<float>& S, const IO<floa
   }
 }
 
-__host__ __device__ constexpr size_t lds_q_bytes() {
-  return wave_tab_bytes<float>() + kQW * q_slice_bytes() + kQE * kQRec * 4 + 16;
+// Two block shapes: QE = 128 envs on QW = 16 waves (the default, two blocks per CU), and QE = 16 envs
+// on QW = 8 waves for small env counts, where 128-env blocks would leave most CUs idle (4 096 envs
+// are 32 such blocks) -- each wave then owns about one pair, and up to four blocks share a CU.
+constexpr int kQE_S = 16, kQW_S = 8;
+constexpr int kQSmallBelow = 32768;   // env count below which the small blocks are the default (tools/nsweep.sh)
+template <int QE = kQE, int QW = kQW> __host__ __device__ constexpr size_t lds_q_bytes() {
+  return wave_tab_bytes<float>() + QW * q_slice_bytes() + QE * kQRec * 4 + 16;
 }
 static_assert(2 * lds_q_bytes() <= 160 * 1024, "two blocks per CU");
+static_assert(4 * lds_q_bytes<kQE_S, kQW_S>() <= 160 * 1024, "four small blocks per CU");
 
-template <int MODE, bool FUSED>
+template <int MODE, bool FUSED, int kQE = ::usv::kQE, int kQW = ::usv::kQW>
 __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<float>& io) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
@@ -1573,7 +1579,8 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
   // first (static) pairs: pair w's rows into wave w's buffer 0.  With the fused dynamics, waves 2 and 3
   // also issue those of waves 0 and 1, whose state loads would otherwise queue behind their own DMA
   // (a wave's loads return in issue order); the barrier below publishes them.
-  constexpr int kDynWaves = FUSED ? kQE / kWave : 0;
+  constexpr int kDynWaves = FUSED ? (kQE + kWave - 1) / kWave : 0;
+  static_assert(kQW >= 2 * kDynWaves && 2 * kQW <= kQE + 2 * kWave, "block shape");
   if (wave >= kDynWaves && cur >= 0) dma_copy1(S.orow(eb + 2 * cur), rowbuf0, min(2, nbe - 2 * cur) * rowb);
   if (FUSED && wave >= kDynWaves && wave < 2 * kDynWaves) {
     const int w = wave - kDynWaves;
@@ -1585,7 +1592,7 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
     // dynamics, one lane per env.  Lanes past the end repeat the wave's last env (same wave:
     // every lane loads the state before any lane stores it); a wave with no env of its own must
     // not run, or two waves would race on the same env's state
-    if (wave < kQE / kWave && wave * kWave < nbe) {
+    if (wave < kDynWaves && wave * kWave < nbe) {
       const int k = min(wave * kWave + l, nbe - 1);
       const int e = eb + k;
       const float2 a = reinterpret_cast<const float2*>(io.act)[e];
@@ -1746,6 +1753,9 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
 template <int MODE, bool FUSED>
 __global__ __launch_bounds__(kQW * kWave) __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8)))
 void step_q_kernel(State<float> S, IO<float> io) { step_q_body<MODE, FUSED>(S, io); }
+template <int MODE>
+__global__ __launch_bounds__(kQW_S * kWave) __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8)))
+void step_qs_kernel(State<float> S, IO<float> io) { step_q_body<MODE, true, kQE_S, kQW_S>(S, io); }
 
 // Split block-queue step, first half: full-width lane-per-env dynamics writing the env records
 // (make_qrec) for step_q_kernel<MODE, false>, plus truncated and the info row.
@@ -2339,8 +2349,9 @@ void* pick_scan(int epw, int lid) {
   return pick_scan_lid<R, MODE, 4, WPB>(lid);
 }
 
-void* pick_q(int mode, bool fused) {
+void* pick_q(int mode, bool fused, bool small = false) {
   const bool simple = mode == USV_MODE_SIMPLE;
+  if (small) return simple ? (void*)&step_qs_kernel<USV_MODE_SIMPLE> : (void*)&step_qs_kernel<USV_MODE_ASMC_SIMPLE>;
   if (fused) return simple ? (void*)&step_q_kernel<USV_MODE_SIMPLE, true> : (void*)&step_q_kernel<USV_MODE_ASMC_SIMPLE, true>;
   return simple ? (void*)&step_q_kernel<USV_MODE_SIMPLE, false> : (void*)&step_q_kernel<USV_MODE_ASMC_SIMPLE, false>;
 }
@@ -2395,8 +2406,10 @@ int launch_step_kernels(Handle* h, State<R>& S, const float* act, float* obs, vo
         void* dyn = simple ? (void*)&dyn_rec_kernel<USV_MODE_SIMPLE> : (void*)&dyn_rec_kernel<USV_MODE_ASMC_SIMPLE>;
         HIP_TRY(hipLaunchKernel(dyn, dim3((S.N + kBlock - 1) / kBlock), dim3(kBlock), args, 0, st));
       }
-      HIP_TRY(hipLaunchKernel(pick_q(h->cfg.mode, h->kind == 5), dim3((S.N + kQE - 1) / kQE), dim3(kQW * kWave),
-                              args, lds_q_bytes(), st));
+      const bool small = h->kind == 5 && h->epb == kQE_S;
+      const int qe = small ? kQE_S : kQE, qw = small ? kQW_S : kQW;
+      HIP_TRY(hipLaunchKernel(pick_q(h->cfg.mode, h->kind == 5, small), dim3((S.N + qe - 1) / qe), dim3(qw * kWave),
+                              args, small ? lds_q_bytes<kQE_S, kQW_S>() : lds_q_bytes(), st));
       return USV_OK;
     }
   }
@@ -2679,14 +2692,15 @@ int usv_create(const usv_config* cfg, int32_t device, void** out) {
     // (45.7 us vs 46.7 for the split wave scan at 65 536 envs)
     if (queue) { h->kind = 4; h->epb = kQE; } else { h->kind = 2; h->epb = 16; }
   } else if (queue) {
-    h->kind = 5; h->epb = kQE;          // block-queue step, 16-wave blocks
+    h->kind = 5;                        // block-queue step: 16-wave blocks of 128 envs, or 8-wave blocks
+    h->epb = cfg->num_envs < kQSmallBelow ? kQE_S : kQE;   // of 16 below kQSmallBelow envs
   } else { h->kind = 1; h->epb = 64; }
   if (const char* v = std::getenv("USV_STEP_VARIANT")) {   // "epb,lid[,kind]" tuning override
     int epb = 0, lid = 0, kind = 0;
     const int got = std::sscanf(v, "%d,%d,%d", &epb, &lid, &kind);
     const bool wave_ok = kind == 1 && (epb == 16 || epb == 32 || epb == 64) && (lid == 0 || lid == 3 || lid == 7);
     const bool split_ok = kind == 2 && (epb == 8 || epb == 16 || epb == 32) && (lid == 0 || lid == 3 || lid == 7);
-    const bool queue_ok = (kind == 4 || kind == 5) && epb == kQE && lid == 7 &&
+    const bool queue_ok = (kind == 4 || kind == 5) && (epb == kQE || (kind == 5 && epb == kQE_S)) && lid == 7 &&
                           cfg->precision == USV_F32 && cfg->obstacle_cap <= 32;
     if (got >= 3 && (wave_ok || split_ok || queue_ok)) {
       h->epb = epb;
@@ -2699,6 +2713,9 @@ int usv_create(const usv_config* cfg, int32_t device, void** out) {
   if (h->kind == 4 || h->kind == 5) {   // the block-queue step's LDS exceeds the 64 KiB default
     HIP_TRY(hipFuncSetAttribute(pick_q(cfg->mode, h->kind == 5), hipFuncAttributeMaxDynamicSharedMemorySize,
                                 (int)lds_q_bytes()));
+    if (h->kind == 5)
+      HIP_TRY(hipFuncSetAttribute(pick_q(cfg->mode, true, true), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds_q_bytes<kQE_S, kQW_S>()));
   }
   const int rc = cfg->precision == USV_F32 ? carve<float>(h, h->sf) : carve<double>(h, h->sd);
   if (rc != USV_OK) {

@@ -342,7 +342,7 @@ def test_step_variants_bit_identical(env_id, precision, monkeypatch):
             + torch.tensor([0.2, -1.0], device="cuda") for _ in range(T)]
     ref = None
     for v in ("64,7,1", "32,0,1", "32,3,1", "16,7,1", "32,7,1", "16,0,2", "32,3,2", "8,7,2", "16,7,2", "32,7,2",
-              "128,7,4", "128,7,5"):
+              "128,7,4", "128,7,5", "16,7,5"):
         monkeypatch.setenv("USV_STEP_VARIANT", v)
         env = make(env_id, n, seed=4, precision=precision)
         env.reset(seed=4)
@@ -369,7 +369,7 @@ def test_block_queue_ragged_sizes(n, monkeypatch):
     acts = [torch.rand(n, 2, device="cuda", generator=gen) * torch.tensor([0.8, 2.0], device="cuda")
             + torch.tensor([0.2, -1.0], device="cuda") for _ in range(T)]
     ref = None
-    for v in ("64,7,1", "128,7,5", "128,7,4", "16,7,2"):
+    for v in ("64,7,1", "128,7,5", "16,7,5", "128,7,4", "16,7,2"):
         monkeypatch.setenv("USV_STEP_VARIANT", v)
         env = make("usv-simple", n, seed=6, max_episode_steps=12)
         env.reset(seed=6)
@@ -403,7 +403,7 @@ def test_step_variants_bit_identical_scattered(precision, monkeypatch):
     assert far.mean() > 0.1, far.mean()          # the far path is actually exercised
     a = torch.from_numpy(rng.uniform([0.2, -1], [1, 1], size=(n, 2)).astype(np.float32)).cuda()
     ref = None
-    for v in ("64,7,1", "32,3,1", "32,7,1", "16,0,1", "16,3,2", "8,7,2", "16,7,2", "128,7,4", "128,7,5"):
+    for v in ("64,7,1", "32,3,1", "32,7,1", "16,0,1", "16,3,2", "8,7,2", "16,7,2", "128,7,4", "128,7,5", "16,7,5"):
         monkeypatch.setenv("USV_STEP_VARIANT", v)
         env = make("usv-simple", n, seed=3, precision=precision)
         inject(env, orc.env, elapsed=1)
