@@ -163,8 +163,8 @@ struct Prof {
 #endif
 // Diagnostic build only (-DUSV_DIAG_QPROF): per-wave shader-clock cycles (s_memtime; its SMEM
 // round trip also waits for the wave's LDS ops, so the marks perturb what they time) spent in each section of the block-queue step, read back with usv_diag_qprof().
-constexpr int kQProfSlots = 12;
 #ifdef USV_DIAG_QPROF
+constexpr int kQProfSlots = 12;
 __device__ unsigned g_qprof[16384 * kQProfSlots];
 __device__ __forceinline__ unsigned shader_cycles() { return (unsigned)__builtin_amdgcn_s_memtime(); }
 struct QProf {
@@ -703,7 +703,7 @@ __device__ __forceinline__ void ray_pair(Ray<R>& ra, R jdx, R jdy, R jr2, R jk, 
 
 // Lidar variants (compile-time): bit 0 = drop obstacles wholly inside the rear blind sector
 // before the ray loop, bit 1 = obstacle loop unrolled by two, bit 2 = angular-window pair
-// expansion (f32 only; f64 uses bits 0|1).  The max-range test of :458 runs only in waves with an
+// expansion (f32: lidar_window / lidar_window2; f64: lidar_window_d).  The max-range test of :458 runs only in waves with an
 // obstacle >= 99 m away (wave-uniform template switch).
 constexpr int kLidSkip = 1, kLidUnroll2 = 2, kLidWindow = 4;
 
@@ -1067,6 +1067,80 @@ __device__ __forceinline__ void lidar_wave2(float* rows, int os, int nl, float p
   lidar_window2(dx, dy, key, d, rr, valid, far, c0r, s0r, reinterpret_cast<float4*>(rows), WinLds{slot, mark, rayoff}, A, B, qp);
 }
 
+// Angular-window lidar for the f64 build (one env per wave).  The ray windows are sized in float from
+// the f64 geometry (the 0.05-ray margin dwarfs the float rounding of the inputs), and every
+// (obstacle, ray) pair in a window runs lidar_brute's exact f64 test on the same ray-0-frame operands
+// (a, b, r^2 and the ray table), so the hits are brute's.  The winner per ray is the smallest key:
+// ds_min_u64 on the order-preserving key bits with the low 6 bits replaced by the obstacle lane, i.e.
+// keys equal to within 64 ulps resolve to the lower lane (brute: exact ties only; the reference's own
+// tie order is unspecified).  The winner's reading is then recomputed exactly as lidar_brute does
+// (reading_of), so readings are bit-identical to the brute loop.
+struct WinLdsD {
+  unsigned long long* slot;   // [128] per wave, armed with kSlotArm between envs
+  int* mark;                  // [64]  per wave
+  const double2* rayoff;      // [128] block-shared ray offset table (f64)
+};
+__device__ __forceinline__ unsigned long long ord_key64(double k) {   // double -> order-preserving u64
+  const unsigned long long b = (unsigned long long)__double_as_longlong(k);
+  return (b >> 63) ? ~b : (b | (1ull << 63));
+}
+template <bool RANGE_CHECK>
+__device__ __forceinline__ void lidar_window_d(double dx, double dy, double key, double d, double rr, bool valid,
+                                               double sp, double cp, const WinLdsD& L, Scan<double>& out) {
+  const int l = lane_id();
+  double a, b;
+  to_ray0(dx, dy, ray_c(cp, sp, double(kStartC), double(kStartS)), ray_s(cp, sp, double(kStartC), double(kStartS)), a, b);
+  const double r2 = rr * rr;
+  const float inv = (float)(1.0 / kRes);
+  float pr = fast_atan2((float)b, (float)a) * inv;    // as lidar_window2: branch cut in the blind sector
+  pr = pr < -32.5f ? pr + 192.0f : pr;
+  const float margin = (float)(kWinMargin * kRes);
+  const float x = fminf((float)rr * __builtin_amdgcn_rcpf((float)d), 1.0f);
+  const float hr = (fmaf((float)(kPi / 2 - 1) * x, x * x, x) + margin) * inv;
+  const bool wide = (d <= rr * 1.001) | (hr >= 32.5f);
+  const int lo = wide ? 0 : max(0, (int)ceilf(pr - hr));
+  const int hi = wide ? 127 : min(127, (int)floorf(pr + hr));
+  const int cnt = valid ? max(0, hi - lo + 1) : 0;
+  const int incl = wave_incl_scan(cnt);
+  const int off = wave_excl_of(incl);
+  const int W = __builtin_amdgcn_readlane(incl, 63);
+  const int mk0 = ((l + 1) << 16) | (lo - off + 32768);
+  const unsigned long long kq = (ord_key64(key) & ~63ull) | (unsigned long long)l;
+  const unsigned kq_lo = (unsigned)kq, kq_hi = (unsigned)(kq >> 32);
+  int carry = 0;
+  for (int base = 0; base < W; base += kWave) {       // wave-uniform pass count
+    L.mark[l] = 0;                                    // (callers' LDS need not be cleared)
+    if (cnt > 0 && off >= base && off < base + kWave) L.mark[off - base] = mk0;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const int mk = max(wave_incl_max_asm(L.mark[l]), carry);
+    carry = __builtin_amdgcn_readlane(mk, 63);
+    const int q = base + l;
+    const int jj = max((mk >> 16) - 1, 0);
+    const int si = (q + (mk & 0xffff) - 32768) & 127;
+    const double ja = __shfl(a, jj, kWave), jb = __shfl(b, jj, kWave), jr2 = __shfl(r2, jj, kWave);
+    const unsigned long long jk = ((unsigned long long)(unsigned)__shfl((int)kq_hi, jj, kWave) << 32) |
+                                  (unsigned)__shfl((int)kq_lo, jj, kWave);
+    const double2 cs = L.rayoff[si];
+    const double proj = m_fma(ja, cs.x, jb * cs.y);    // ray_pair's arithmetic
+    const double perp = m_fma(ja, cs.y, -(jb * cs.x));
+    const double delta = m_fma(-perp, perp, jr2);
+    bool hit = (q < W) & (proj >= 0.0) & (delta >= 0.0);
+    if (RANGE_CHECK) hit = hit && (proj - l_sqrt(delta)) < double(kSensorMax);   // :458
+    if (hit) atomicMin(&L.slot[si], jk);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  const unsigned long long v0 = L.slot[l], v1 = L.slot[l + 64];
+  L.slot[l] = kSlotArm;
+  L.slot[l + 64] = kSlotArm;
+  L.mark[l] = 0;
+  const int bj0 = v0 == kSlotArm ? -1 : (int)(v0 & 63), bj1 = v1 == kSlotArm ? -1 : (int)(v1 & 63);
+  const double2 t0 = L.rayoff[l], t1 = L.rayoff[l + 64];
+  out.rd0 = reading_of(t0.x, t0.y, bj0, a, b, r2);
+  out.rd1 = reading_of(t1.x, t1.y, bj1, a, b, r2);
+}
+
 template <typename R, int LID, typename Row>
 __device__ __forceinline__ void lidar_wave(const Row& E, int n, R px, R py, R sp, R cp,
                                            const typename Vec2<R>::T* rayoff, unsigned long long* slot,
@@ -1084,6 +1158,12 @@ __device__ __forceinline__ void lidar_wave(const Row& E, int n, R px, R py, R sp
     const WinLds W{slot, mark, rayoff};
     if (!out.far) lidar_window<false>(dx, dy, key, d, rr, valid, px, py, sp, cp, W, E, out);
     else lidar_window<true>(dx, dy, key, d, rr, valid, px, py, sp, cp, W, E, out);
+    return;
+  }
+  if constexpr (std::is_same<R, double>::value && (LID & kLidWindow) != 0) {
+    const WinLdsD W{slot, mark, rayoff};
+    if (!out.far) lidar_window_d<false>(dx, dy, key, d, rr, valid, sp, cp, W, out);
+    else lidar_window_d<true>(dx, dy, key, d, rr, valid, sp, cp, W, out);
     return;
   }
   const auto t0 = rayoff[l], t1 = rayoff[l + 64];
