@@ -136,6 +136,11 @@ class UsvVectorEnv:
             self._check(self.lib.usv_set_reset_rng(self._h, _lib.RESET_NUMPY_PCG64))
         self.info_enabled = bool(info) and env_id not in LEGACY_IDS   # the legacy ids return {}
         self.info_buf = torch.zeros((n, _lib.INFO_DIM), dtype=torch.float32, **kw) if self.info_enabled else None
+        # step() hot path: the persistent buffers' pointers and bool views, made once
+        self._out_ptrs = (_ptr(self.obs), _ptr(self.reward), _ptr(self._term), _ptr(self._trunc),
+                          _ptr(self.final_obs), _ptr(self.info_buf))
+        self._term_b, self._trunc_b = self._term.view(torch.bool), self._trunc.view(torch.bool)
+        self._done_b = torch.zeros(n, dtype=torch.bool, **kw)
         self.options = dict(options or {})
         unknown = set(self.options) - {"run_custom_experiment", "experiment"}
         if unknown:
@@ -227,19 +232,21 @@ class UsvVectorEnv:
         return self.obs, (self._info_dict(reset=True) if self.info_enabled else {})
 
     def step(self, actions):
-        a = torch.as_tensor(actions, device=self.device)
+        if isinstance(actions, torch.Tensor) and actions.device == self.device:
+            a = actions
+        else:
+            a = torch.as_tensor(actions, device=self.device)
         if a.dtype != torch.float32 or not a.is_contiguous():
             a = a.to(torch.float32).contiguous()
         if self.act_dim == 1 and a.shape == (self.num_envs,):
             a = a.reshape(self.num_envs, 1)
         if a.shape != (self.num_envs, self.act_dim):
             raise ValueError(f"actions must be [{self.num_envs}, {self.act_dim}], got {tuple(a.shape)}")
-        self._check(self.lib.usv_step_ex(self._h, _ptr(a), _ptr(self.obs), _ptr(self.reward),
-                                        _ptr(self._term), _ptr(self._trunc), _ptr(self.final_obs),
-                                        _ptr(self.info_buf), _stream_ptr(self.device)))
-        term = self._term.view(torch.bool)
-        trunc = self._trunc.view(torch.bool)
-        info = {"final_obs": self.final_obs, "_final_obs": term | trunc}
+        o, r, te, tr, fo, inf = self._out_ptrs
+        self._check(self.lib.usv_step_ex(self._h, ctypes.c_void_p(a.data_ptr()), o, r, te, tr, fo, inf,
+                                        _stream_ptr(self.device)))
+        term, trunc = self._term_b, self._trunc_b
+        info = {"final_obs": self.final_obs, "_final_obs": torch.bitwise_or(term, trunc, out=self._done_b)}
         if self.info_enabled:
             info.update(self._info_dict())
         return self.obs, self.reward, term, trunc, info
