@@ -87,3 +87,16 @@ def test_vector_env_fails_loudly_without_gpu():
     import gym_usv_amd
     with pytest.raises(gym_usv_amd.UsvLibError):
         gym_usv_amd.make_vec("usv-simple", 8)
+
+
+def test_safe_vmcnt_build_same_abi():
+    """libusvhip_safe.so (the vmcnt(0) debug build the GPU tests compare bitwise with the product)
+    exports the same C-ABI and loads side by side with the product library (own ctypes handle)."""
+    from gym_usv_amd import _lib
+    from gym_usv_amd.build import build_all
+    build_all(verbose=False)
+    prod, safe = _lib.load(), _lib.load(_lib.SAFE_LIB_PATH)
+    assert prod is not safe and _lib.load(_lib.SAFE_LIB_PATH) is safe
+    assert safe.usv_abi_version() == prod.usv_abi_version() == _lib.ABI_VERSION
+    for name in _declared_functions():
+        assert hasattr(safe, name), name
