@@ -120,6 +120,12 @@ __device__ unsigned long long g_stamps[32768 * kStampSlots];
     if ((threadIdx.x & 63) == 0 && gw_ < 32768)                                           \
       g_stamps[gw_ * kStampSlots + (i)] = __builtin_amdgcn_s_memrealtime();               \
   } while (0)
+// a wave slot holding a value instead of a time
+#define USV_STAMP_V(i, v)                                                                 \
+  do {                                                                                    \
+    const unsigned gw_ = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;               \
+    if ((threadIdx.x & 63) == 0 && gw_ < 32768) g_stamps[gw_ * kStampSlots + (i)] = (v);  \
+  } while (0)
 // slot 7: HW_ID (SIMD, CU, SE bits) | XCC_ID << 32 of the wave
 #define USV_STAMP_ID()                                                                    \
   do {                                                                                    \
@@ -133,6 +139,7 @@ __device__ unsigned long long g_stamps[32768 * kStampSlots];
 #define USV_STAMP(i) do {} while (0)
 #define USV_STAMP_B(i) do {} while (0)
 #define USV_STAMP_W(i) do {} while (0)
+#define USV_STAMP_V(i, v) do {} while (0)
 #endif
 // Diagnostic build only (-DUSV_DIAG_PROF): per-wave shader-clock (s_memtime) cycles spent in
 // each part of the wave-per-env scan, read back with usv_diag_prof().  Never in the product.
@@ -1826,6 +1833,7 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
   }
   QMARK(11);
   qprof_flush(qp);
+  USV_STAMP_V(4, (unsigned long long)it);            // (diagnostic: pairs this wave scanned)
   USV_STAMP_W(3);
   USV_STAMP_W(6);
 }

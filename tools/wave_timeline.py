@@ -114,6 +114,27 @@ def main():
             out["younger_has_larger_block_id"] = round(float(np.mean([p[1][2] > p[0][2] for p in pairs])), 3)
             out["younger_id_ge_half_grid"] = round(float(np.mean([p[1][2] >= nw // wpb // 2 for p in pairs])), 3)
             out["older_ends_first"] = round(float(np.mean(older_end <= younger_end)), 3)
+        # per CU: first wave start, last wave end; which CUs set the launch's end
+        cus = sorted(per_cu)
+        cs = np.array([min(x[0] for x in per_cu[c]) for c in cus])
+        ce = np.array([max(x[1] for x in per_cu[c]) for c in cus])
+        out["cu_start_us"], out["cu_end_us"], out["cu_busy_us"] = pct(cs), pct(ce), pct(ce - cs)
+        out["corr_cu_start_end"] = round(float(np.corrcoef(cs, ce)[0, 1]), 3)
+        cx = np.array(cus) // 128
+        out["cu_end_by_xcc"] = {int(x): [round(float(ce[cx == x].mean()), 2), round(float(ce[cx == x].max()), 2)]
+                                for x in np.unique(cx)}
+        out["cu_start_by_xcc"] = {int(x): round(float(cs[cx == x].mean()), 2) for x in np.unique(cx)}
+        out["cu_busy_by_xcc"] = {int(x): round(float((ce - cs)[cx == x].mean()), 2) for x in np.unique(cx)}
+        oe = np.array([min(x[1] for x in per_cu[c]) - min(x[0] for x in per_cu[c]) for c in cus])
+        out["older_busy_by_xcc"] = {int(x): round(float(oe[cx == x].mean()), 2) for x in np.unique(cx)}
+        cse = np.array(cus) // 16
+        out["cu_end_by_se_mean"] = pct([ce[cse == q].mean() for q in np.unique(cse)])
+        slow = np.argsort(-ce)[:8]
+        out["slowest_cus"] = [[int(cus[i]), round(float(cs[i]), 2),
+                               [round(x[1] - x[0], 2) for x in sorted(per_cu[cus[i]])],
+                               round(float(ce[i]), 2)] for i in slow]
+        pairs_w = raw[:, 4].astype(np.int64)
+        out["pairs_per_wave"] = pct(pairs_w)
     print(json.dumps(out))
 
 
