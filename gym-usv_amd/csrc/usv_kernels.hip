@@ -874,6 +874,13 @@ __device__ __forceinline__ int wave_incl_max(int v) {
 // The same scan as fused DPP maxes in one asm block: a lane whose row is masked off by row_bcast keeps
 // its value (vdst = src1), so no zero-filled temporaries are needed.  s_nop 1 before each DPP read
 // of the VGPR the previous VALU wrote (gfx9 DPP hazard).
+// floor(x) converted to int in one instruction (|x| well inside the int range here)
+__device__ __forceinline__ int cvt_flr_i32(float x) {
+  int r;
+  asm("v_cvt_flr_i32_f32 %0, %1" : "=v"(r) : "v"(x));
+  return r;
+}
+
 __device__ __forceinline__ int wave_incl_max_asm(int v) {
   asm volatile("s_nop 1\n\t"
                "v_max_i32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\ts_nop 1\n\t"
@@ -989,35 +996,44 @@ __device__ __forceinline__ void lidar_window2(float dx, float dy, float key, flo
   const float x = fminf(rr * __builtin_amdgcn_rcpf(d), 1.0f);
   // asin(x) <= x + (pi/2 - 1) x^3 (see lidar_window); boat inside: all rays
   const float hr = (fmaf((float)(kPi / 2 - 1) * x, x * x, x) + margin) * inv;
-  const bool wide = (d <= rr * 1.001f) | (hr >= 32.5f);
-  const int lo = wide ? 0 : max(0, (int)ceilf(pr - hr));
-  const int hi = wide ? 127 : min(127, (int)floorf(pr + hr));
+  // all rays when the window reaches 32 rays: that includes the boat inside the obstacle (x = 1
+  // gives hr = 32.05), and a narrower window never wraps onto the rays.  ceil(v) = -floor(-v)
+  // (v_cvt_flr_i32_f32: floor and convert in one instruction)
+  const bool wide = hr >= 32.0f;
+  const int lo = wide ? 0 : max(0, -cvt_flr_i32(hr - pr));
+  const int hi = wide ? 127 : min(127, cvt_flr_i32(pr + hr));
   const int cnt = valid ? max(0, hi - lo + 1) : 0;
   const int incl = wave_incl_scan(cnt);
   const int off = wave_excl_of(incl);
   const int W = __builtin_amdgcn_readlane(incl, 63);
   // Segment marks: obstacle lane l's run of pairs starts at off and maps pair q to slot
   // q + (lo - off) + 128 [env B], i.e. ray (slot & 127).  Its mark, written at off, is
-  // (l + 1) << 16 | (lo - off + 128 [env B] + 32768): the owner in the high bits keeps the max-scan in
+  // l << 16 | (lo - off + 128 [env B] + 32768): the owner in the high bits keeps the max-scan in
   // run order and the slot offset rides in the low bits (in [24704, 33023]), so a pair finds its
   // owner, its ray and its slot from one max-scan, with no per-pair gather of the owner's window.
-  const int mk0 = ((l + 1) << 16) | (lo - off + (l >= 32 ? 128 : 0) + 32768);
+  // A cleared mark is 0, below every mark (the low bits are > 0), and pair 0 always has one (the
+  // first obstacle with pairs starts at 0), so every pair's scan result names an owner.
+  const int mk0 = (l << 16) | (lo - off + (l >= 32 ? 128 : 0) + 32768);
   rec[l] = make_float4(a, b, rr * rr, __uint_as_float(ord_key(key)));
   // The marks are cleared once per call (below), not per pass: a mark left by an earlier pass of
   // this call is <= that pass's carry, which the max-scan folds in anyway.
+  // the pass that holds this obstacle's mark (-1: no pairs) and the mark's index in it
+  const int mpass = cnt > 0 ? off >> 6 : -1;
+  int* const mslot = L.mark + (off & (kWave - 1));
   int carry = 0;
   QMARK(2);
-  for (int base = 0; base < W; base += kWave) {       // wave-uniform pass count
+  for (int base = 0, pass = 0; base < W; base += kWave, ++pass) {   // wave-uniform pass count
     QCOUNT(9, 1);
-    if (cnt > 0 && off >= base && off < base + kWave) L.mark[off - base] = mk0;
+    if (mpass == pass) *mslot = mk0;
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");   // marks and records visible
     __builtin_amdgcn_wave_barrier();
     const int mk = max(wave_incl_max_asm(L.mark[l]), carry);
     carry = __builtin_amdgcn_readlane(mk, 63);
-    const int q = base + l;
-    const int jj = max((mk >> 16) - 1, 0);            // owner obstacle lane
-    // slot of (owner env, ray): exact for q < W; other lanes (no hit) read some ray's offsets
-    const int si = q + (mk & 0xffff) - 32768;
+    const int jj = mk >> 16;                          // owner obstacle lane
+    // slot of (owner env, ray) of pair q = base + l: q + (mk & 0xffff) - 32768, of which only the
+    // low 8 bits are used (= those of q + mk); exact for q < W, other lanes (no hit) read some
+    // ray's offsets
+    const int si = base + l + mk;
     const float4 o = rec[jj];                         // owner's (a, b, r^2, key bits)
     const float2 cs = L.rayoff[si & 127];
     // the key half of the payload before the hit branch (the whole record is read by one
@@ -1029,7 +1045,7 @@ __device__ __forceinline__ void lidar_window2(float dx, float dy, float key, flo
     const float perp = fmaf(o.x, cs.y, -(o.y * cs.x));
     const float delta = fmaf(-perp, perp, o.z);
     const float dist = proj - l_sqrt(delta);
-    const bool hit = (q < W) & (proj >= 0.0f) & (delta >= 0.0f) & (!far | (dist < (float)kSensorMax));  // :458
+    const bool hit = (l < W - base) & (proj >= 0.0f) & (delta >= 0.0f) & (!far | (dist < (float)kSensorMax));  // :458
     if (hit)                                          // slots: env A's rays, then env B's
       atomicMin(sl, ((unsigned long long)kb << 32) | __float_as_uint(dist));
   }
