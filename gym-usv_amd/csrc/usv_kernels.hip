@@ -1640,7 +1640,10 @@ __device__ __forceinline__ void q_emit_done(const State<float>& S, const IO<floa
 // Two block shapes: QE = 128 envs on QW = 16 waves (the default, two blocks per CU), and QE = 16 envs
 // on QW = 8 waves for small env counts, where 128-env blocks would leave most CUs idle (4 096 envs
 // are 32 such blocks) -- each wave then owns about one pair, and up to four blocks share a CU.
-constexpr int kQE_S = 16, kQW_S = 8;
+#ifndef USV_QE_S
+#define USV_QE_S 16      // envs per small block (diagnostic builds may change it)
+#endif
+constexpr int kQE_S = USV_QE_S, kQW_S = 8;
 constexpr int kQSmallBelow = 32768;   // env count below which the small blocks are the default (tools/nsweep.sh)
 template <int QE = kQE, int QW = kQW> __host__ __device__ constexpr size_t lds_q_bytes() {
   return wave_tab_bytes<float>() + QW * q_slice_bytes() + QE * kQRec * 4 + 16;
