@@ -1575,7 +1575,16 @@ __global__ __launch_bounds__(kWave * WPB) void scan_kernel(State<R> S, IO<R> io)
 #ifndef USV_QE
 #define USV_QE 128       // envs per block-queue block (diagnostic builds may change it)
 #endif
-constexpr int kQW = 16, kQE = USV_QE, kQRec = 16;
+#ifndef USV_QW
+#define USV_QW 16        // waves per block-queue block (diagnostic builds may change it)
+#endif
+#ifndef USV_QSGPR
+#define USV_QSGPR 80     // SGPR budget of the block-queue kernel (80: 8 waves per SIMD)
+#endif
+#ifndef USV_QWPE
+#define USV_QWPE 8       // waves per SIMD it is compiled for
+#endif
+constexpr int kQW = USV_QW, kQE = USV_QE, kQRec = 16;
 __host__ __device__ constexpr size_t q_slice_bytes() { return 256 * 8 + 64 * 4 + 2 * 1024; }
 
 // One DMA instruction (<= 64 pieces of 16 B, i.e. <= 1 KiB): pieces c >= nchunk are not copied.
@@ -1858,7 +1867,7 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
 }
 
 template <int MODE, bool FUSED>
-__global__ __launch_bounds__(kQW * kWave) __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8)))
+__global__ __launch_bounds__(kQW * kWave) __attribute__((amdgpu_num_sgpr(USV_QSGPR), amdgpu_waves_per_eu(USV_QWPE, USV_QWPE)))
 void step_q_kernel(State<float> S, IO<float> io) { step_q_body<MODE, FUSED>(S, io); }
 template <int MODE>
 __global__ __launch_bounds__(kQW_S * kWave) __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8)))
