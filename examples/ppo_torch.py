@@ -176,7 +176,7 @@ class PPO:
 
 def train(env_id="usv-simple", envs=4096, updates=10, n_steps=16, batch_size=4096, seed=0, log=print):
     import gym_usv_amd
-    env = gym_usv_amd.make_vec(env_id, envs, seed=seed)
+    env = gym_usv_amd.make_vec(env_id, envs, seed=seed, copy=False)   # each step is consumed at once
     ppo = PPO(env, n_steps=n_steps, batch_size=batch_size, seed=seed)
     hist = []
     t0 = time.perf_counter()

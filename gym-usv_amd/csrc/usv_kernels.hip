@@ -86,7 +86,7 @@ template <typename R> struct IO {
   uint8_t* trunc;          // [N]
   float* fobs;             // [N][143] or null
   const uint8_t* mask;     // [N] or null (reset kernel)
-  float* info;             // [N][USV_INFO_DIM] or null: step info (step kernels) / reset info
+  R* info;                 // [N][USV_INFO_DIM] in R (f32 / f64 build) or null: step info (step kernels) / reset info
   int kpath;               // reset kernel: options['place_obstacles_on_path'] (0 = none)
 };
 
@@ -97,99 +97,19 @@ constexpr int kLidDefault = 7;  // lidar variant of the reset kernel (all varian
 
 template <typename R> __device__ __forceinline__ R big() { return R(1e30); }
 
-// Diagnostic build only (-DUSV_DIAG_STAMPS): per-block s_memrealtime (100 MHz) stamps at the
-// phase boundaries of the step kernel, read back with usv_diag_stamps().  Never in the product.
-#ifdef USV_DIAG_STAMPS
-constexpr int kStampSlots = 8;
-__device__ unsigned long long g_stamps[32768 * kStampSlots];
-#define USV_STAMP(i)                                                                      \
-  do {                                                                                    \
-    if (threadIdx.x == 0 && blockIdx.x < 32768)                                           \
-      g_stamps[blockIdx.x * kStampSlots + (i)] = __builtin_amdgcn_s_memrealtime();        \
-  } while (0)
-// block slot, written by the first lane of whichever wave executes it (kind 0)
-#define USV_STAMP_B(i)                                                                    \
-  do {                                                                                    \
-    if ((threadIdx.x & 63) == 0 && blockIdx.x < 32768)                                    \
-      g_stamps[blockIdx.x * kStampSlots + (i)] = __builtin_amdgcn_s_memrealtime();        \
-  } while (0)
-// wave slot (global wave index; kinds 1-3)
-#define USV_STAMP_W(i)                                                                    \
-  do {                                                                                    \
-    const unsigned gw_ = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;               \
-    if ((threadIdx.x & 63) == 0 && gw_ < 32768)                                           \
-      g_stamps[gw_ * kStampSlots + (i)] = __builtin_amdgcn_s_memrealtime();               \
-  } while (0)
-// a wave slot holding a value instead of a time
-#define USV_STAMP_V(i, v)                                                                 \
-  do {                                                                                    \
-    const unsigned gw_ = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;               \
-    if ((threadIdx.x & 63) == 0 && gw_ < 32768) g_stamps[gw_ * kStampSlots + (i)] = (v);  \
-  } while (0)
-// slot 7: HW_ID (SIMD, CU, SE bits) | XCC_ID << 32 of the wave
-#define USV_STAMP_ID()                                                                    \
-  do {                                                                                    \
-    const unsigned gw_ = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;               \
-    const unsigned long long hw_ = __builtin_amdgcn_s_getreg((31 << 11) | 4);             \
-    const unsigned long long xcc_ = __builtin_amdgcn_s_getreg((15 << 11) | 20);           \
-    if ((threadIdx.x & 63) == 0 && gw_ < 32768) g_stamps[gw_ * kStampSlots + 7] = hw_ | (xcc_ << 32); \
-  } while (0)
+#ifdef USV_DIAG
+#include "usv_diag.hpp"       // diagnostic builds only: per-block / per-wave clock stamps
 #else
 #define USV_STAMP_ID() do {} while (0)
 #define USV_STAMP(i) do {} while (0)
 #define USV_STAMP_B(i) do {} while (0)
 #define USV_STAMP_W(i) do {} while (0)
 #define USV_STAMP_V(i, v) do {} while (0)
-#endif
-// Diagnostic build only (-DUSV_DIAG_PROF): per-wave shader-clock (s_memtime) cycles spent in
-// each part of the wave-per-env scan, read back with usv_diag_prof().  Never in the product.
-#ifdef USV_DIAG_PROF
-constexpr int kProfWaves = 16384, kProfSlots = 8;
-__device__ unsigned long long g_prof[kProfWaves * kProfSlots];
-struct Prof {
-  unsigned long long acc[kProfSlots] = {};
-  unsigned long long t;
-  __device__ Prof() : t(__builtin_amdgcn_s_memtime()) {}
-  __device__ void mark(int i) {
-    const unsigned long long n = __builtin_amdgcn_s_memtime();
-    acc[i] += n - t;
-    t = n;
-  }
-  __device__ void count(int i) { acc[i] += 1; }
-  __device__ void flush(int gw) {
-    if ((threadIdx.x & 63) == 0 && gw < kProfWaves)
-      for (int k = 0; k < kProfSlots; ++k) g_prof[gw * kProfSlots + k] = acc[k];
-  }
-};
-#else
 struct Prof {
   __device__ void mark(int) {}
   __device__ void count(int) {}
   __device__ void flush(int) {}
 };
-#endif
-// Diagnostic build only (-DUSV_DIAG_QPROF): per-wave shader-clock cycles (s_memtime; its SMEM
-// round trip also waits for the wave's LDS ops, so the marks perturb what they time) spent in each section of the block-queue step, read back with usv_diag_qprof().
-#ifdef USV_DIAG_QPROF
-constexpr int kQProfSlots = 12;
-__device__ unsigned g_qprof[16384 * kQProfSlots];
-__device__ __forceinline__ unsigned shader_cycles() { return (unsigned)__builtin_amdgcn_s_memtime(); }
-struct QProf {
-  unsigned acc[kQProfSlots];
-  unsigned t;
-  __device__ QProf() : t(shader_cycles()) { for (int i = 0; i < kQProfSlots; ++i) acc[i] = 0; }
-  __device__ __forceinline__ void mark(int i) { const unsigned n = shader_cycles(); acc[i] += n - t; t = n; }
-  __device__ __forceinline__ void count(int i, unsigned k = 1) { acc[i] += k; }
-  __device__ void flush() {
-    const unsigned gw = blockIdx.x * (blockDim.x / 64) + threadIdx.x / 64;
-    if ((threadIdx.x & 63) == 0 && gw < 16384)
-      for (int k = 0; k < kQProfSlots; ++k) g_qprof[gw * kQProfSlots + k] = acc[k];
-  }
-};
-#define QMARK(i) do { if (qp) qp->mark(i); } while (0)
-__device__ __forceinline__ void qprof_flush(QProf* qp) { qp->flush(); }
-#define QCOUNT(i, k) do { if (qp) qp->count(i, k); } while (0)
-#else
 struct QProf { __device__ void mark(int) {} __device__ void count(int, unsigned = 1) {} __device__ void flush() {} };
 #define QMARK(i) do {} while (0)
 #define QCOUNT(i, k) do {} while (0)
@@ -254,11 +174,10 @@ __device__ __forceinline__ void philox_uniforms(Philox& g, int l, Uni4<double>& 
 
 // Reset info row _get_info(-1, zeros(3)) (simple_env.py:102-115, :305); reward terms 0.
 template <typename R>
-__device__ __forceinline__ void reset_info(float* info, R x, R y, R psi, R u, R v, R r, R px0, R py0,
-                                           R px1, R py1, R ye, float angle_n) {
-  const float vals[USV_INFO_DIM] = {(float)x, (float)y, (float)psi, (float)u, (float)v, (float)r,
-                                    (float)px0, (float)py0, (float)px1, (float)py1, 0.0f, 0.0f,
-                                    (float)ye, angle_n, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+__device__ __forceinline__ void reset_info(R* info, R x, R y, R psi, R u, R v, R r, R px0, R py0,
+                                           R px1, R py1, R ye, R angle_n) {
+  const R vals[USV_INFO_DIM] = {x, y, psi, u, v, r, px0, py0, px1, py1, R(0), R(0),
+                                ye, angle_n, R(0), R(0), R(0), R(0), R(0), R(0), R(0), R(0)};
 #pragma unroll
   for (int i = 0; i < USV_INFO_DIM; ++i) info[i] = vals[i];
 }
@@ -279,7 +198,7 @@ __device__ __forceinline__ R path_ye(R x, R y, R x0, R y0, R x1, R y1) {
 // the reset kernel after reset_wave and, for same-step autoresets, by exp_autoreset_kernel after
 // the step (kept out of the step kernels, whose pair loop it would make spill).
 template <typename R>
-__device__ __forceinline__ void reset_experiment(const State<R>& S, int e, int ep, float* row, float* info) {
+__device__ __forceinline__ void reset_experiment(const State<R>& S, int e, int ep, float* row, R* info) {
   const R* X = S.exp;
   R tx, ty, u, v, r, mu, mr, refv;
   {
@@ -316,11 +235,11 @@ __device__ __forceinline__ void reset_experiment(const State<R>& S, int e, int e
   float h[kHdr];
   make_header<R>(h, u, v, r, angle, dst, ye, refv, R(0), R(0), mu, mr);
   for (int i = 0; i < kHdr; ++i) row[i] = h[i];
-  if (info) reset_info<R>(info, px, py, psi, u, v, r, ps0, ps1, pe0, pe1, ye, h[3]);
+  if (info) reset_info<R>(info, px, py, psi, u, v, r, ps0, ps1, pe0, pe1, ye, cdiv(angle, kPi));
 }
 
 template <typename R, int MODE>
-__device__ __forceinline__ void reset_wave(const State<R>& S, int e, float* row, float* info = nullptr,
+__device__ __forceinline__ void reset_wave(const State<R>& S, int e, float* row, R* info = nullptr,
                                            int kpath = 0) {
   if (S.np_reset) return;                  // NumPy-exact mode: np_autoreset_kernel resets after the step
   const int l = lane_id();
@@ -403,7 +322,7 @@ __device__ __forceinline__ void reset_wave(const State<R>& S, int e, float* row,
     make_header<R>(h, u, v, r, angle, dst, R(0), refv, R(0), R(0), mu, mr);
 #pragma unroll
     for (int i = 0; i < kHdr; ++i) row[i] = h[i];
-    if (info) reset_info<R>(info, sx, sy, psi, u, v, r, sx, sy, sx + ca * dist, sy + sa * dist, R(0), h[3]);
+    if (info) reset_info<R>(info, sx, sy, psi, u, v, r, sx, sy, sx + ca * dist, sy + sa * dist, R(0), cdiv(angle, kPi));
   }
 }
 
@@ -492,7 +411,7 @@ __device__ __forceinline__ void np_store(const State<R>& S, int e, const NpPcg64
 // zeroes the ASMC state (simple_env_asmc.py:14-16).  Writes the reset obs header into `row`
 // (its sensor half, the stale scan, is the caller's).  Draws in double, stored as R.
 template <typename R, int MODE>
-__device__ void np_reset(const State<R>& S, int e, float* row, float* info = nullptr, int kpath = 0) {
+__device__ void np_reset(const State<R>& S, int e, float* row, R* info = nullptr, int kpath = 0) {
   NpPcg64 g = np_load(S, e);
   const double sx = 0.5 * g.standard_normal() + kBound / 2;                      // :234-235
   const double sy = 0.5 * g.standard_normal() + kBound / 2;
@@ -563,7 +482,7 @@ __device__ void np_reset(const State<R>& S, int e, float* row, float* info = nul
   float h[kHdr];
   make_header<R>(h, R(u), R(v), R(r), angle, dst, ye, R(refv), R(0), R(0), R(mu), R(mr));
   for (int i = 0; i < kHdr; ++i) row[i] = h[i];
-  if (info) reset_info<R>(info, x0, y0, ps, R(u), R(v), R(r), R(ps0), R(ps1), R(pe0), R(pe1), ye, h[3]);
+  if (info) reset_info<R>(info, x0, y0, ps, R(u), R(v), R(r), R(ps0), R(ps1), R(pe0), R(pe1), ye, cdiv(angle, kPi));
 }
 
 // Same-step autoreset in NumPy-exact mode, after the step kernel: envs that ended this step get
@@ -590,7 +509,7 @@ __global__ __launch_bounds__(kBlock) void exp_autoreset_kernel(State<R> S, IO<R>
 // Also returns sin/cos of the new heading so the wave-per-env lidar does not recompute them.
 template <typename R, int MODE>
 __device__ void env_dynamics(const State<R>& S, int e, float a_u, float a_r, float (&hdr)[kHdr],
-                             R& px, R& py, R& psp, R& pcp, R& partial, bool& trunc, float* info = nullptr) {
+                             R& px, R& py, R& psp, R& pcp, R& partial, bool& trunc, R* info = nullptr) {
   R x = S.F(F_X)[e], y = S.F(F_Y)[e], psi = S.F(F_PSI)[e];
   R u = S.F(F_U)[e], v = S.F(F_V)[e], r = S.F(F_R)[e];
   const int el0 = S.I(I_ELAPSED)[e];
@@ -653,11 +572,8 @@ __device__ void env_dynamics(const State<R>& S, int e, float a_u, float a_r, flo
   const R dact_r = -(dact / R(2)) * R(0.15);
   partial = ye_r + ang_r + vel_r + dact_r;
   if (info) {                                        // _get_info + reward_info (:102-115, :189-199)
-    const float vals[USV_INFO_DIM] = {
-        (float)x, (float)y, (float)psi, (float)u, (float)v, (float)r, (float)x0, (float)y0,
-        (float)S.F(F_PX1)[e], (float)S.F(F_PY1)[e], (float)a3u, (float)a3r, (float)ye, hdr[3],
-        (float)ye_r, (float)ang_r, (float)dact_r, (float)dact, (float)vel_r, (float)refv, (float)lu,
-        (float)(lu - refv)};
+    const R vals[USV_INFO_DIM] = {x, y, psi, u, v, r, x0, y0, S.F(F_PX1)[e], S.F(F_PY1)[e], a3u, a3r, ye,
+                                  cdiv(angle, kPi), ye_r, ang_r, dact_r, dact, vel_r, refv, lu, lu - refv};
 #pragma unroll
     for (int i = 0; i < USV_INFO_DIM; ++i) info[i] = vals[i];
   }
@@ -1325,12 +1241,8 @@ __device__ __forceinline__ void emit_env(const State<R>& S, const IO<R>& io, int
   coll_m |= (unsigned)coll << k;
   const float s0 = (float)l_norm(sc.rd0), s1 = (float)l_norm(sc.rd1);        // :82-83
   float* row = io.obs + (size_t)e * kObsDim;
-#ifdef USV_ABL_NOSTORE   // diagnostic ablation only: sensor half of the obs row not written
-  if (s0 == 12345.0f) row[kHdr + l] = s1;
-#else
   row[kHdr + l] = s0;                                          // stale scan is kept by reset
   row[kHdr + 64 + l] = s1;
-#endif
   if (done) {
     if (io.fobs) {                                             // terminal obs
       float* f = io.fobs + (size_t)e * kObsDim;
@@ -1453,13 +1365,8 @@ __device__ __forceinline__ void step_body_wave(const State<R>& S, const IO<R>& i
     const int e = e0 + min(l, ne - 1);
     const float2 a = reinterpret_cast<const float2*>(io.act)[e];
     float hdr[kHdr];
-#ifdef USV_ABL_NODYN     // diagnostic ablation only: pose from x, y, action; no dynamics
-    px = S.F(F_X)[e]; py = S.F(F_Y)[e]; sp = R(a.x); cp = R(a.y); partial = R(0); trunc = false;
-    for (int i = 0; i < kHdr; ++i) hdr[i] = (float)px;
-#else
     env_dynamics<R, MODE>(S, e, a.x, a.y, hdr, px, py, sp, cp, partial, trunc,
                              io.info ? io.info + (size_t)e * USV_INFO_DIM : nullptr);
-#endif
     float* row = io.obs + (size_t)e * kObsDim;
 #pragma unroll
     for (int i = 0; i < kHdr; ++i) row[i] = hdr[i];
@@ -1599,16 +1506,9 @@ __device__ __forceinline__ void dma_copy1(const void* src, void* dst, int bytes)
                       (uint64_t)(unsigned)__builtin_amdgcn_readfirstlane((unsigned)a);
   if (c < bytes / 16) {
     unsigned keep;
-#ifdef USV_DMA_VADDR      // (diagnostic: per-lane 64-bit address form)
-    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-                 "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-                 : "=&s"(keep) : "v"(reinterpret_cast<const char*>(src) + 16 * (size_t)c), "s"(d) : "memory");
-    (void)sb;
-#else
     asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
                  "global_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
                  : "=&s"(keep) : "v"(16 * c), "s"(sb), "s"(d) : "memory");
-#endif
   }
 }
 
@@ -1714,13 +1614,8 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
       float hdr[kHdr];
       float px, py, sp, cp, partial;
       bool trunc;
-#ifdef USV_ABL_NODYN     // diagnostic ablation only: pose from x, y, action; no dynamics
-      px = S.F(F_X)[e]; py = S.F(F_Y)[e]; sp = a.x; cp = a.y; partial = 0.0f; trunc = false;
-      for (int i = 0; i < kHdr; ++i) hdr[i] = px;
-#else
       env_dynamics<float, MODE>(S, e, a.x, a.y, hdr, px, py, sp, cp, partial, trunc,
                                 io.info ? io.info + (size_t)e * USV_INFO_DIM : nullptr);
-#endif
       io.trunc[e] = trunc;
       make_qrec(recs + k * kQRec, px, py, sp, cp, partial, S.I(I_NOBS)[e], trunc, hdr);
     }
@@ -1787,14 +1682,9 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
       const int el = e0 + (kl - k0);
       const int nt = __float_as_int(meta.y);
       Scan<float> sa, sb;
-#ifdef USV_ABL_NOLIDAR   // diagnostic ablation only: readings from the row and pose, no scan
-      sa.rd0 = cbuf[l & 31] + pose.x; sa.rd1 = pose.y + pose.z; sa.term = sa.far = false;
-      sb = sa;
-#else
       QMARK(1);
       lidar_wave2(cbuf, os, (hb && !hasB) ? 0 : (nt & 0xffff), pose.x, pose.y, pose.z, pose.w, rayoff, slot,
                   mark, sa, sb, qp);
-#endif
       float4 pose_n = pose, meta_n = meta;
       float hv_n = hv;
       if (nxt >= 0) rec_of(nxt, pose_n, meta_n, hv_n);   // the next pair's record (wave-uniform)
@@ -1809,7 +1699,6 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
       const bool termB = hasB ? sb.term : sa.term;
       float* const rowA = io.obs + (size_t)e0 * kObsDim;
       float* const rowB = rowA + (hasB ? kObsDim : 0);
-#ifndef USV_ABL_NOSTORE   // (diagnostic ablation: obs rows not written)
       rowA[kHdr + l] = l_norm(sa.rd0);                  // sensors (:82-83)
       rowA[kHdr + 64 + l] = l_norm(sa.rd1);
       rowB[kHdr + l] = l_norm(sB0);
@@ -1820,7 +1709,6 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
         const float hc = hi == 12 ? (float)(kMaxAccU / 10.0) : hi == 14 ? (float)(kMaxAccR / 10.0) : 0.0f;
         rowA[(hB ? kObsDim : 0) + hi] = ((hpk >> 17) & 1) ? hc : hv;
       }
-#endif
       const bool term_l = hb ? termB : sa.term;         // reward, terminated: lanes 0..31 env A,
       const bool coll_l = hb ? collB : collA;           // 32..63 env B
       io.rew[el] = coll_l ? -20.0f + meta.x : meta.x;
@@ -1834,11 +1722,7 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
       // the next pair's rows landed: at least seven stores (four sensor halves, the headers, the
       // rewards and the terminated flags) were issued after their DMA
       QMARK(5);
-#ifdef USV_ABL_NOSTORE
-      vm_wait<2>();
-#else
       vm_wait<7>();
-#endif
       QMARK(6);
       cur = nxt;
       pose = pose_n;
@@ -1937,7 +1821,7 @@ __global__ __launch_bounds__(kBlock) void reset_kernel(State<R> S, IO<R> io) {
     float* row = io.obs + (size_t)e * kObsDim;
     row[kHdr + l] = (float)l_norm(rd0);
     row[kHdr + 64 + l] = (float)l_norm(rd1);
-    float* info = io.info ? io.info + (size_t)e * USV_INFO_DIM : nullptr;
+    R* info = io.info ? io.info + (size_t)e * USV_INFO_DIM : nullptr;
     if (S.np_reset) {
       if (l == 0) np_reset<R, MODE>(S, e, row, info, io.kpath);
     } else {
@@ -2474,12 +2358,12 @@ void* pick_q(int mode, bool fused, bool small = false) {
 
 template <typename R>
 int launch_step_kernels(Handle* h, State<R>& S, const float* act, float* obs, void* rew, uint8_t* term,
-                        uint8_t* trunc, float* fobs, float* info, hipStream_t st);
+                        uint8_t* trunc, float* fobs, void* info, hipStream_t st);
 
 // The step, then (NumPy-exact reset mode) the resets of the envs that ended in it.
 template <typename R>
 int launch_step(Handle* h, State<R>& S, const float* act, float* obs, void* rew, uint8_t* term,
-                uint8_t* trunc, float* fobs, float* info, hipStream_t st) {
+                uint8_t* trunc, float* fobs, void* info, hipStream_t st) {
   const int rc = launch_step_kernels(h, S, act, obs, rew, term, trunc, fobs, info, st);
   // (the legacy kernels reset inline, from the MT19937 state, in the NumPy-exact mode too)
   if (rc != USV_OK || S.autoreset != USV_AUTORESET_SAME_STEP || is_legacy(h->cfg.mode)) return rc;
@@ -2500,8 +2384,8 @@ int launch_step(Handle* h, State<R>& S, const float* act, float* obs, void* rew,
 
 template <typename R>
 int launch_step_kernels(Handle* h, State<R>& S, const float* act, float* obs, void* rew, uint8_t* term,
-                        uint8_t* trunc, float* fobs, float* info, hipStream_t st) {
-  IO<R> io{act, obs, (R*)rew, term, trunc, fobs, nullptr, is_legacy(h->cfg.mode) ? nullptr : info, 0};
+                        uint8_t* trunc, float* fobs, void* info, hipStream_t st) {
+  IO<R> io{act, obs, (R*)rew, term, trunc, fobs, nullptr, is_legacy(h->cfg.mode) ? nullptr : (R*)info, 0};
   if (is_legacy(h->cfg.mode)) {
     const dim3 grid((S.N + kBlock - 1) / kBlock), block(kBlock);
     if (h->cfg.mode == USV_MODE_ASMC_V0)
@@ -2545,9 +2429,9 @@ int launch_step_kernels(Handle* h, State<R>& S, const float* act, float* obs, vo
 }
 
 template <typename R>
-int launch_reset(Handle* h, State<R>& S, const uint8_t* mask, float* obs, int kpath, float* info,
+int launch_reset(Handle* h, State<R>& S, const uint8_t* mask, float* obs, int kpath, void* info,
                  hipStream_t st) {
-  IO<R> io{nullptr, obs, nullptr, nullptr, nullptr, nullptr, mask, is_legacy(h->cfg.mode) ? nullptr : info, kpath};
+  IO<R> io{nullptr, obs, nullptr, nullptr, nullptr, nullptr, mask, is_legacy(h->cfg.mode) ? nullptr : (R*)info, kpath};
   const dim3 grid((S.N + kEPBReset - 1) / kEPBReset), block(kBlock);
   const dim3 lgrid((S.N + kBlock - 1) / kBlock);
   if (h->cfg.mode == USV_MODE_ASMC_V0)
@@ -2726,6 +2610,17 @@ int set_experiment(Handle* h, State<R>& S, const usv_experiment* x) {
   return USV_OK;
 }
 
+// The block-queue step's LDS exceeds the 64 KiB default: raise the kernels' dynamic-LDS limit.
+int queue_lds_attr(const Handle* h) {
+  if (h->kind != 4 && h->kind != 5) return USV_OK;
+  HIP_TRY(hipFuncSetAttribute(pick_q(h->cfg.mode, h->kind == 5), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds_q_bytes()));
+  if (h->kind == 5)
+    HIP_TRY(hipFuncSetAttribute(pick_q(h->cfg.mode, true, true), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                (int)lds_q_bytes<kQE_S, kQW_S>()));
+  return USV_OK;
+}
+
 Handle* as_handle(void* p) { return static_cast<Handle*>(p); }
 
 }  // namespace
@@ -2811,28 +2706,8 @@ int usv_create(const usv_config* cfg, int32_t device, void** out) {
     h->kind = 5;                        // block-queue step: 16-wave blocks of 128 envs, or 8-wave blocks
     h->epb = cfg->num_envs < kQSmallBelow ? kQE_S : kQE;   // of 16 below kQSmallBelow envs
   } else { h->kind = 1; h->epb = 64; }
-  if (const char* v = std::getenv("USV_STEP_VARIANT")) {   // "epb,lid[,kind]" tuning override
-    int epb = 0, lid = 0, kind = 0;
-    const int got = std::sscanf(v, "%d,%d,%d", &epb, &lid, &kind);
-    const bool wave_ok = kind == 1 && (epb == 16 || epb == 32 || epb == 64) && (lid == 0 || lid == 3 || lid == 7);
-    const bool split_ok = kind == 2 && (epb == 8 || epb == 16 || epb == 32) && (lid == 0 || lid == 3 || lid == 7);
-    const bool queue_ok = (kind == 4 || kind == 5) && (epb == kQE || (kind == 5 && epb == kQE_S)) && lid == 7 &&
-                          cfg->precision == USV_F32 && cfg->obstacle_cap <= 32;
-    if (got >= 3 && (wave_ok || split_ok || queue_ok)) {
-      h->epb = epb;
-      h->lid = lid;
-      h->kind = kind;
-    }
-  }
   h->prio = (h->kind == 4 || h->kind == 5) ? 0 : 1;   // the ramp helps static splits only
-  if (const char* v = std::getenv("USV_PRIO")) h->prio = std::atoi(v);   // tuning override
-  if (h->kind == 4 || h->kind == 5) {   // the block-queue step's LDS exceeds the 64 KiB default
-    HIP_TRY(hipFuncSetAttribute(pick_q(cfg->mode, h->kind == 5), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)lds_q_bytes()));
-    if (h->kind == 5)
-      HIP_TRY(hipFuncSetAttribute(pick_q(cfg->mode, true, true), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)lds_q_bytes<kQE_S, kQW_S>()));
-  }
+  if (const int rc = queue_lds_attr(h); rc != USV_OK) { delete h; return rc; }
   const int rc = cfg->precision == USV_F32 ? carve<float>(h, h->sf) : carve<double>(h, h->sd);
   if (rc != USV_OK) {
     if (h->slab) (void)hipFree(h->slab);
@@ -2841,6 +2716,26 @@ int usv_create(const usv_config* cfg, int32_t device, void** out) {
   }
   *out = h;
   return USV_OK;
+}
+
+int usv_set_kernel_variant(void* hp, int32_t kind, int32_t epb, int32_t lid) {
+  Handle* h = as_handle(hp);
+  if (!h) return fail(USV_ERR_ARG, "null handle");
+  if (is_legacy(h->cfg.mode)) return fail(USV_ERR_ARG, "the legacy ids have one lane-per-env kernel");
+  const usv_config* cfg = &h->cfg;
+  const bool lid_ok = lid == 0 || lid == 3 || lid == 7;
+  const bool wave_ok = kind == 1 && (epb == 16 || epb == 32 || epb == 64) && lid_ok;
+  const bool split_ok = kind == 2 && (epb == 8 || epb == 16 || epb == 32) && lid_ok;
+  const bool queue_ok = (kind == 4 || kind == 5) && (epb == kQE || (kind == 5 && epb == kQE_S)) && lid == 7 &&
+                        cfg->precision == USV_F32 && cfg->obstacle_cap <= 32;
+  if (!(wave_ok || split_ok || queue_ok)) return fail(USV_ERR_ARG, "kernel variant not available for this config");
+  DeviceGuard g(h->device);
+  HIP_TRY(hipDeviceSynchronize());                 // launches in flight keep the variant they took
+  h->kind = kind;
+  h->epb = epb;
+  h->lid = lid;
+  h->prio = (kind == 4 || kind == 5) ? 0 : 1;
+  return queue_lds_attr(h);
 }
 
 void usv_destroy(void* hp) {
@@ -2885,7 +2780,7 @@ int usv_seed(void* hp, uint64_t seed) {
   return USV_OK;
 }
 
-int usv_reset_ex(void* hp, const uint8_t* mask, float* obs, const usv_reset_options* opt, float* info,
+int usv_reset_ex(void* hp, const uint8_t* mask, float* obs, const usv_reset_options* opt, void* info,
                  void* stream) {
   Handle* h = as_handle(hp);
   if (!h || !obs) return fail(USV_ERR_ARG, "null argument");
@@ -2906,7 +2801,7 @@ int usv_reset(void* hp, const uint8_t* mask, float* obs, void* stream) {
 }
 
 int usv_step_ex(void* hp, const float* act, float* obs, void* rew, uint8_t* term, uint8_t* trunc,
-                float* fobs, float* info, void* stream) {
+                float* fobs, void* info, void* stream) {
   Handle* h = as_handle(hp);
   if (!h || !act || !obs || !rew || !term || !trunc) return fail(USV_ERR_ARG, "null argument");
   DeviceGuard g(h->device);

@@ -14,7 +14,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 # diagnostic builds (tools/) may point at another in-tree copy of the library
 LIB_PATH = os.environ.get("USV_LIB_PATH", LIB_PATH)
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 MODE_SIMPLE, MODE_ASMC_SIMPLE, MODE_ASMC_V0, MODE_ASMC_YE_INT_V0, MODE_PID_V0 = 0, 1, 2, 3, 4
 F32, F64 = 0, 1
 AUTORESET_SAME_STEP, AUTORESET_DISABLED = 0, 1
@@ -81,6 +81,7 @@ SIGNATURES = [
     ("usv_state_bytes", _sz, [_vp]),
     ("usv_get_state", ctypes.c_int, [_vp, _vp, _sz]),
     ("usv_set_state", ctypes.c_int, [_vp, _vp, _sz]),
+    ("usv_set_kernel_variant", ctypes.c_int, [_vp, _i32, _i32, _i32]),
 ]
 
 _LIBS = {}

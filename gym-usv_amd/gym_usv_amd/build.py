@@ -66,7 +66,10 @@ def build_library(force=False, verbose=True, variant="product"):
 
 
 def build_all(force=False, verbose=True):
-    """Every variant, compiled concurrently (one hipcc process each)."""
+    """Every variant, compiled concurrently (one hipcc process each).  Every job is waited for; the
+    variants that compiled are installed even if another failed (the product library does not depend
+    on the vmcnt(0) debug build), failed jobs leave no temporary output, and the first failure is
+    raised at the end."""
     jobs = []
     for v in VARIANTS:
         out, cmd = _cmd(v)
@@ -74,10 +77,17 @@ def build_all(force=False, verbose=True):
             if verbose:
                 print(" ".join(cmd), flush=True)
             jobs.append((out, subprocess.Popen(cmd)))
+    failed = []
     for out, p in jobs:
-        if p.wait() != 0:
-            raise subprocess.CalledProcessError(p.returncode, "hipcc " + out)
-        os.replace(out + ".tmp", out)
+        if p.wait() == 0:
+            os.replace(out + ".tmp", out)
+        else:
+            failed.append((p.returncode, out))
+            if os.path.exists(out + ".tmp"):
+                os.remove(out + ".tmp")
+    if failed:
+        rc, out = failed[0]
+        raise subprocess.CalledProcessError(rc, "hipcc " + out)
 
 
 if __name__ == "__main__":

@@ -4,11 +4,12 @@
 (gym_usv/envs/simple_env.py:7, simple_env_asmc.py:7): ``reset(seed=None, options=None) ->
 (obs float32[143], info)`` and ``step(action) -> (obs, reward, terminated, truncated, info)``
 with NumPy in/out.  Each is a 1-env ``UsvVectorEnv`` with autoreset off and no TimeLimit
-(``gym_usv_amd.make`` adds the registered TimeLimit, like ``gymnasium.make``).  With
-``reset_rng="numpy"`` a usv-simple / usv-asmc-simple env draws its resets from
-``Generator(PCG64(SeedSequence(seed)))`` exactly like the reference, so ``reset(seed=s)`` followed by
-the same actions reproduces the reference's episode.  They exist for
-API compatibility and debugging; throughput lives in ``UsvVectorEnv``.
+(``gym_usv_amd.make`` adds the registered TimeLimit, like ``gymnasium.make``).  By default
+(``reset_rng="numpy"``) a usv-simple / usv-asmc-simple env draws its resets from
+``Generator(PCG64(SeedSequence(seed)))`` exactly like the reference (the legacy ids from np.random's
+MT19937 after ``np.random.seed(seed)``), so ``make(id).reset(seed=s)`` followed by the same actions
+reproduces the reference's episode; ``reset_rng="philox"`` selects the in-kernel Philox resets of the
+vector env.  They exist for API compatibility and debugging; throughput lives in ``UsvVectorEnv``.
 """
 from __future__ import annotations
 
@@ -23,7 +24,7 @@ class _SingleEnv:
     metadata = {"render_modes": [], "render_fps": 30}
 
     def __init__(self, render_mode=None, options=None, device=0, precision="f32",
-                 max_episode_steps=0, seed=None, reset_rng="philox", obstacle_cap=32, perturb=False):
+                 max_episode_steps=0, seed=None, reset_rng="numpy", obstacle_cap=32, perturb=False):
         if render_mode not in (None, "rgb_array"):
             raise NotImplementedError("render_mode 'human' (a pygame window) is out of scope; use 'rgb_array'")
         self.render_mode = render_mode

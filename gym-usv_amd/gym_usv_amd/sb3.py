@@ -92,6 +92,8 @@ class Sb3VecEnv:
     def __init__(self, env_id="usv-simple", num_envs=4096, frame_stack=0, seed=0, venv=None, **kw):
         if venv is None:
             from .vector_env import UsvVectorEnv
+            # each step is consumed (copied to the host) before the next: the persistent buffers do
+            kw.setdefault("copy", False)
             venv = UsvVectorEnv(env_id, num_envs=num_envs, seed=seed, autoreset=True, **kw)
         self.venv = venv
         self.num_envs = venv.num_envs

@@ -10,6 +10,7 @@ observation in ``info["final_obs"]``), and the TimeLimit of the registered id
 from __future__ import annotations
 
 import ctypes
+import warnings
 
 import numpy as np
 import torch
@@ -77,9 +78,12 @@ class UsvVectorEnv:
     reset(seed=None, options=None, mask=None) -> (obs [N,143] f32, info)
     step(actions [N,2] f32)  -> (obs, reward [N], terminated [N] bool, truncated [N] bool, info)
 
-    Returned tensors are the env's own device buffers (zero-copy); they are overwritten by the
-    next call — clone them to keep them.  ``info["final_obs"]`` holds the terminal obs rows of
-    envs that ended this step (``info["_final_obs"]`` is the mask).
+    ``copy=True`` (default, gymnasium's ``SyncVectorEnv(copy=True)`` convention): every call returns
+    tensors of its own -- the kernel writes straight into freshly allocated device tensors, so this
+    costs no extra copy.  ``copy=False``: the env's persistent device buffers are returned and the next
+    call overwrites them (no allocation; for loops that consume each step before the next).
+    ``info["final_obs"]`` holds the terminal obs rows of envs that ended this step
+    (``info["_final_obs"]`` is the mask; rows where it is False are unspecified).
     """
 
     metadata = {"render_modes": [], "autoreset_mode": "same-step"}
@@ -87,11 +91,13 @@ class UsvVectorEnv:
     def __init__(self, env_id="usv-simple", num_envs=4096, device=0, seed=0, precision="f32",
                  autoreset=True, max_episode_steps=None, obstacle_cap=32, lidar="window",
                  env_id_offset=0, reset_rng="philox", options=None, info=False, perturb=False,
-                 lib_path=None):
+                 copy=True, kernel_variant=None, lib_path=None):
         """``options`` are UsvSimpleEnv's constructor options (simple_env.py:10): only
         ``run_custom_experiment`` / ``experiment`` (:292-300) exist there.  ``info=True`` returns the
         reference's per-step info keys (simple_env.py:102-115, 189-199) as device tensors.
-        ``perturb=True`` runs usv-asmc-simple's UsvAsmc.compute with do_perturb (usv_asmc.py:184-199)."""
+        ``perturb=True`` runs usv-asmc-simple's UsvAsmc.compute with do_perturb (usv_asmc.py:184-199).
+        ``kernel_variant="epb,lid,kind"`` selects a step-kernel variant (usv_set_kernel_variant; all
+        variants give bit-identical outputs, the GPU tests compare them); None = the tuned default."""
         if env_id not in ENV_SPECS:
             raise ValueError(f"unknown env id {env_id!r}; known: {sorted(ENV_SPECS)}")
         if not torch.cuda.is_available():
@@ -115,10 +121,15 @@ class UsvVectorEnv:
         with torch.cuda.device(self.device):
             self._check(self.lib.usv_create(ctypes.byref(cfg), self.device.index, ctypes.byref(h)))
         self._h = h
+        if kernel_variant is not None:
+            epb, lid, kind = (int(v) for v in str(kernel_variant).split(","))
+            self._check(self.lib.usv_set_kernel_variant(h, kind, epb, lid))
         n = self.num_envs
         self.obs_dim = self.lib.usv_obs_dim(h)
         self.act_dim = self.lib.usv_act_dim(h)
         rdt = torch.float32 if precision == "f32" else torch.float64
+        self._rdt = rdt
+        self.copy = bool(copy)
         kw = dict(device=self.device)
         self.obs = torch.zeros((n, self.obs_dim), dtype=torch.float32, **kw)
         self.final_obs = torch.zeros((n, self.obs_dim), dtype=torch.float32, **kw)
@@ -135,21 +146,24 @@ class UsvVectorEnv:
         if reset_rng == "numpy":
             self._check(self.lib.usv_set_reset_rng(self._h, _lib.RESET_NUMPY_PCG64))
         self.info_enabled = bool(info) and env_id not in LEGACY_IDS   # the legacy ids return {}
-        self.info_buf = torch.zeros((n, _lib.INFO_DIM), dtype=torch.float32, **kw) if self.info_enabled else None
+        # info rows in the handle's precision (f64 build: float64 rows, like the reference's values)
+        self.info_buf = torch.zeros((n, _lib.INFO_DIM), dtype=rdt, **kw) if self.info_enabled else None
         # step() hot path: the persistent buffers' pointers and bool views, made once
         self._out_ptrs = (_ptr(self.obs), _ptr(self.reward), _ptr(self._term), _ptr(self._trunc),
                           _ptr(self.final_obs), _ptr(self.info_buf))
         self._term_b, self._trunc_b = self._term.view(torch.bool), self._trunc.view(torch.bool)
-        self._done_b = torch.zeros(n, dtype=torch.bool, **kw)
+        self._last_obs = self.obs              # the latest obs rows (a masked reset keeps the others)
+        self._last_rew = self.reward
         self.options = dict(options or {})
+        # the reference reads only these keys and ignores any other (simple_env.py:292)
         unknown = set(self.options) - {"run_custom_experiment", "experiment"}
         if unknown:
-            raise ValueError(f"unknown constructor options {sorted(unknown)} (UsvSimpleEnv reads only "
-                             "'run_custom_experiment' and 'experiment', simple_env.py:292-300)")
-        if self.options and env_id != "usv-simple":
-            raise ValueError("constructor options exist for usv-simple only (UsvSimpleASMCEnv.__init__ takes "
-                             "none, simple_env_asmc.py:10)")
+            warnings.warn(f"constructor options {sorted(unknown)} are ignored (UsvSimpleEnv reads only "
+                          "'run_custom_experiment' and 'experiment', simple_env.py:292-300)", stacklevel=2)
         if self.options.get("run_custom_experiment"):
+            if env_id != "usv-simple":
+                raise ValueError("run_custom_experiment exists for usv-simple only (UsvSimpleASMCEnv.__init__ "
+                                 "takes no options, simple_env_asmc.py:10)")
             self.set_experiment(self.options["experiment"])
 
     def _check(self, rc):
@@ -177,35 +191,39 @@ class UsvVectorEnv:
         x.position[0], x.position[1], x.position[2] = p3
         self._check(self.lib.usv_set_experiment(self._h, ctypes.byref(x)))
 
-    def _info_dict(self, reset=False):
-        """The reference's info keys as device tensors (views of the info buffer)."""
-        b, n = self.info_buf, self.num_envs
+    def _info_dict(self, b, reward=None, reset=False, mask=None):
+        """The reference's info keys as device tensors (views of the info rows ``b``).  After a reset
+        the reward is -1 (_get_info(-1, ...), simple_env.py:305) in the rows of the reset envs; rows of
+        envs a masked reset left alone keep their last values."""
+        n = self.num_envs
+        if reset:
+            rew = torch.full((n,), -1.0, dtype=self._rdt, device=self.device)
+            if mask is not None:
+                rew = torch.where(mask, rew, self._last_rew)
+        else:
+            rew = reward
         col = {k: i for i, k in enumerate(_lib.INFO_KEYS)}
+        z = torch.zeros(n, dtype=self._rdt, device=self.device)
         d = {"position": b[:, 0:3], "velocity": b[:, 3:6], "path_start": b[:, 6:8], "path_end": b[:, 8:10],
-             "reward": torch.full((n,), -1.0, device=self.device) if reset else self.reward,
-             "action0": b[:, col["action0"]], "action1": b[:, col["action1"]],
-             "left_thruster": torch.zeros(n, device=self.device), "right_thruster": torch.zeros(n, device=self.device),
+             "reward": rew, "action0": b[:, col["action0"]], "action1": b[:, col["action1"]],
+             "left_thruster": z, "right_thruster": z,
              "ye": b[:, col["ye"]], "angle_to_target": b[:, col["angle_to_target"]]}
         if not reset:
             for k in ("ye_reward", "angle_to_target_reward", "delta_action_reward", "delta_action",
                       "velocity_track_reward", "reference_velocity", "reward_velocity", "reference_velocity_error"):
                 d[k] = b[:, col[k]]
-            d["angle_action_reward"] = torch.zeros(n, device=self.device)
+            d["angle_action_reward"] = z
         return d
 
     # ------------------------------------------------------------------ API
     def reset(self, seed=None, options=None, mask=None):
         """UsvSimpleEnv.reset (simple_env.py:228-308) for every env (or those where ``mask``);
-        ``options={'place_obstacles_on_path': k}`` (:276-288) needs ``obstacle_cap >= 29 + k``."""
-        opts = dict(options or {})
-        unknown = set(opts) - {"place_obstacles_on_path"}
-        if unknown:
-            raise ValueError(f"unknown reset options {sorted(unknown)} (simple_env.py:276 reads only "
-                             "'place_obstacles_on_path')")
+        ``options={'place_obstacles_on_path': k}`` (:276-288) needs ``obstacle_cap >= 29 + k``.
+        Other option keys are ignored, as the reference ignores them; UsvSimpleASMCEnv.reset drops its
+        options altogether (simple_env_asmc.py:14-16: super().reset(seed=seed))."""
         ropt = _lib.UsvResetOptions()
-        # UsvSimpleASMCEnv.reset drops its options (simple_env_asmc.py:14-16: super().reset(seed=seed))
-        if self.env_id == "usv-simple":
-            ropt.place_obstacles_on_path = int(opts.get("place_obstacles_on_path") or 0)
+        if self.env_id == "usv-simple" and options:
+            ropt.place_obstacles_on_path = int(dict(options).get("place_obstacles_on_path") or 0)
         if self.reset_rng == "numpy":
             # each env owns a numpy Generator(PCG64(SeedSequence(seed_i))), like gymnasium's
             # Env.reset(seed) (simple_env.py:229); an int seed gives env i seed + global id (the
@@ -227,9 +245,18 @@ class UsvVectorEnv:
         m = None
         if mask is not None:
             m = torch.as_tensor(mask, device=self.device).to(torch.uint8).contiguous()
-        self._check(self.lib.usv_reset_ex(self._h, _ptr(m), _ptr(self.obs), ctypes.byref(ropt),
-                                         _ptr(self.info_buf), _stream_ptr(self.device)))
-        return self.obs, (self._info_dict(reset=True) if self.info_enabled else {})
+        # rows of envs that are not reset keep the latest obs (and info) rows
+        obs = self._last_obs.clone() if self.copy else self._last_obs
+        ib = self.info_buf
+        if self.info_enabled and self.copy:
+            ib = self.info_buf.clone()
+        self._check(self.lib.usv_reset_ex(self._h, _ptr(m), _ptr(obs), ctypes.byref(ropt),
+                                         _ptr(ib), _stream_ptr(self.device)))
+        self._last_obs = obs
+        if not self.info_enabled:
+            return obs, {}
+        self.info_buf = ib
+        return obs, self._info_dict(ib, reset=True, mask=None if m is None else m.bool())
 
     def step(self, actions):
         if isinstance(actions, torch.Tensor) and actions.device == self.device:
@@ -242,14 +269,30 @@ class UsvVectorEnv:
             a = a.reshape(self.num_envs, 1)
         if a.shape != (self.num_envs, self.act_dim):
             raise ValueError(f"actions must be [{self.num_envs}, {self.act_dim}], got {tuple(a.shape)}")
-        o, r, te, tr, fo, inf = self._out_ptrs
+        if self.copy:
+            # fresh outputs: the kernel writes every row of obs / reward / flags (and of the info rows),
+            # so new tensors cost an allocation, not a copy
+            n, dev = self.num_envs, self.device
+            obs = torch.empty((n, self.obs_dim), dtype=torch.float32, device=dev)
+            fobs = torch.empty((n, self.obs_dim), dtype=torch.float32, device=dev)
+            rew = torch.empty(n, dtype=self._rdt, device=dev)
+            flags = torch.empty((2, n), dtype=torch.bool, device=dev)
+            term, trunc = flags[0], flags[1]
+            ib = torch.empty_like(self.info_buf) if self.info_enabled else None
+            ptrs = (_ptr(obs), _ptr(rew), _ptr(term), _ptr(trunc), _ptr(fobs), _ptr(ib))
+        else:
+            obs, rew, fobs, ib = self.obs, self.reward, self.final_obs, self.info_buf
+            term, trunc = self._term_b, self._trunc_b
+            ptrs = self._out_ptrs
+        o, r, te, tr, fo, inf = ptrs
         self._check(self.lib.usv_step_ex(self._h, ctypes.c_void_p(a.data_ptr()), o, r, te, tr, fo, inf,
                                         _stream_ptr(self.device)))
-        term, trunc = self._term_b, self._trunc_b
-        info = {"final_obs": self.final_obs, "_final_obs": torch.bitwise_or(term, trunc, out=self._done_b)}
+        self._last_obs, self._last_rew = obs, rew
+        info = {"final_obs": fobs, "_final_obs": term | trunc}
         if self.info_enabled:
-            info.update(self._info_dict())
-        return self.obs, self.reward, term, trunc, info
+            self.info_buf = ib
+            info.update(self._info_dict(ib, rew))
+        return obs, rew, term, trunc, info
 
     def step_raw(self, actions, obs, reward, term, trunc, final_obs=None, stream=None):
         """Launch one step into caller-owned buffers (no checks, no allocation): bench / graphs."""
@@ -295,7 +338,7 @@ class UsvVectorEnv:
         names = ("x", "y", "psi", "path_x0", "path_y0", "path_x1", "path_y1", "progress", "n_obs",
                  "obs_x", "obs_y", "obs_r")
         f = {k: self.get_field(k) for k in names}
-        return frame_from_state(f, i, self.obs[i].detach().cpu().numpy(), window_size)
+        return frame_from_state(f, i, self._last_obs[i].detach().cpu().numpy(), window_size)
 
     def get_state(self):
         """All per-env state as {field: ndarray} (env checkpoint / parity inspection)."""

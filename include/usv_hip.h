@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define USV_ABI_VERSION 2
+#define USV_ABI_VERSION 3
 #define USV_SENSOR_COUNT 128
 #define USV_OBS_DIM 143      /* 15 + 128, simple_env.py:27 */
 #define USV_ACT_DIM 2        /* simple_env.py:30 */
@@ -114,7 +114,8 @@ typedef enum usv_flags {
   USV_FLAG_PERTURB = 1
 } usv_flags;
 
-/* Per-step info (opt-in, usv_step_ex / usv_reset_ex): one f32 row of USV_INFO_DIM values per env,
+/* Per-step info (opt-in, usv_step_ex / usv_reset_ex): one row of USV_INFO_DIM values per env, in the
+ * handle's precision (f32, or f64 for USV_F64: usv_reward_bytes gives the element size),
  * the keys of UsvSimpleEnv._get_info + reward_info (gym_usv/envs/simple_env.py:102-115,189-199).
  * "reward" is rew_dev itself; keys that are constant in the reference (left/right_thruster = 0,
  * angle_action_reward = 0) are not stored.  After an explicit reset the row is
@@ -215,9 +216,9 @@ int usv_set_reset_rng(void* handle, int32_t kind);
  * reset observation rows into obs_dev [num_envs][obs_dim] (other rows untouched). */
 int usv_reset(void* handle, const uint8_t* mask_dev, float* obs_dev, void* stream);
 /* usv_reset with reset options (NULL = none) and an optional info buffer info_dev
- * [num_envs][USV_INFO_DIM] f32 (NULL = none; rows of reset envs are written). */
+ * [num_envs][USV_INFO_DIM] f32 / f64 by precision (NULL = none; rows of reset envs are written). */
 int usv_reset_ex(void* handle, const uint8_t* mask_dev, float* obs_dev,
-                 const usv_reset_options* options, float* info_dev, void* stream);
+                 const usv_reset_options* options, void* info_dev, void* stream);
 /* Install (experiment != NULL) or remove (NULL) the custom experiment of every env. */
 int usv_set_experiment(void* handle, const usv_experiment* experiment);
 
@@ -231,11 +232,22 @@ int usv_set_experiment(void* handle, const usv_experiment* experiment);
  *                 (rows of envs not done are left untouched). */
 int usv_step(void* handle, const float* act_dev, float* obs_dev, void* rew_dev,
              uint8_t* term_dev, uint8_t* trunc_dev, float* final_obs_dev, void* stream);
-/* usv_step that also writes the per-step info rows into info_dev [num_envs][USV_INFO_DIM] f32
- * (usv-simple / usv-asmc-simple; the legacy *-v0 ids return {} in the reference and ignore it). */
+/* usv_step that also writes the per-step info rows into info_dev [num_envs][USV_INFO_DIM] f32 / f64
+ * by precision (usv-simple / usv-asmc-simple; the legacy *-v0 ids return {} in the reference and
+ * ignore it). */
 int usv_step_ex(void* handle, const float* act_dev, float* obs_dev, void* rew_dev,
-                uint8_t* term_dev, uint8_t* trunc_dev, float* final_obs_dev, float* info_dev,
+                uint8_t* term_dev, uint8_t* trunc_dev, float* final_obs_dev, void* info_dev,
                 void* stream);
+
+/* Select the step-kernel variant of a usv-simple / usv-asmc-simple handle (verification and
+ * tuning: every variant computes bit-identical outputs, tests/test_gpu_*.py compare them bitwise).
+ * No reference counterpart; usv_create picks the tuned default.
+ *   kind 1: fused wave kernel (epb 16 | 32 | 64 envs per 256-thread block)
+ *   kind 2: split dynamics + wave scan (epb 8 | 16 | 32)
+ *   kind 4 / 5: split / fused block-queue step (epb 128; kind 5 also 16), f32 window lidar, cap <= 32
+ *   lid: lidar variant bits (0 brute, 3 brute + blind-sector skip + unroll, 7 angular window)
+ * Waits for in-flight launches first.  USV_ERR_ARG if the handle's config cannot run it. */
+int usv_set_kernel_variant(void* handle, int32_t kind, int32_t epb, int32_t lid);
 
 /* Field metadata: values per env, 1 if int32, name. */
 int usv_field_info(void* handle, int32_t field, int32_t* per_env, int32_t* is_int,

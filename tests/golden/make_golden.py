@@ -290,12 +290,14 @@ def gen_asmc_perturb(E, n_env=6, T=160, fname="asmc_perturb_traj.npz"):
     print(fname, "+ compute sequences", d["compute_seq"].shape)
 
 
-def gen_info_traj(E, n_env=4, T=64, fname="simple_info_traj.npz"):
+def gen_info_traj(E, n_env=4, T=64, fname="simple_info_traj.npz", cls=None, seed0=5000):
     """usv-simple rollouts (as gen_traj, TimeLimit 500) recording the reset and step info dicts
-    (simple_env.py:102-115, 189-199, 305)."""
-    rng = np.random.default_rng(17)
+    (simple_env.py:102-115, 189-199, 305).  ``cls`` = UsvSimpleASMCEnv records usv-asmc-simple's,
+    which is UsvSimpleEnv.step's info after the two ASMC computes (simple_env_asmc.py:18-27)."""
+    cls = cls or E.UsvSimpleEnv
+    rng = np.random.default_rng(17 + seed0 - 5000)
     acts = np.stack([rng.uniform([0.2, -1], [1, 1], size=(T, 2)) for _ in range(n_env)]).astype(np.float32)
-    seeds = np.arange(n_env) + 5000
+    seeds = np.arange(n_env) + seed0
     out = {"obs0": np.zeros((n_env, 143), np.float32), "final_obs": np.zeros((n_env, T, 143), np.float32),
            "reward": np.zeros((n_env, T)), "terminated": np.zeros((n_env, T), bool),
            "truncated": np.zeros((n_env, T), bool)}
@@ -309,7 +311,7 @@ def gen_info_traj(E, n_env=4, T=64, fname="simple_info_traj.npz"):
         out["info0_" + k] = np.zeros(n_env)
     st0 = []
     for e in range(n_env):
-        env = E.UsvSimpleEnv(render_mode=None)
+        env = cls(render_mode=None)
         o, inf = env.reset(seed=int(seeds[e]))
         out["obs0"][e] = o
         st0.append(snapshot(env))
@@ -384,9 +386,61 @@ def gen_experiment(E, fname="experiment.npz", T=40):
     print(fname, "steps until end:", (term | trunc).argmax(axis=1))
 
 
+# --------------------------------------------------------------------------- round-3 fixtures
+def snapshot_full(env, cap=CAP2):
+    """Everything the step reads, with room for 29 + k obstacles: the state-injection image."""
+    n = env.obstacle_n
+    ox, oy, r = np.zeros(cap), np.zeros(cap), np.zeros(cap)
+    ox[:n], oy[:n], r[:n] = env.obstacle_positions[:, 0], env.obstacle_positions[:, 1], env.obstacle_radius
+    return dict(position=np.array(env.position, dtype=np.float64), velocity=np.array(env.velocity, dtype=np.float64),
+                last_action=np.array(env.last_action, dtype=np.float64), progress=float(env.progress),
+                path_start=np.array(env.path_start, dtype=np.float64), path_end=np.array(env.path_end, dtype=np.float64),
+                target=np.array(env.target_position, dtype=np.float64),
+                max_action=np.array(env.max_action, dtype=np.float64), ref_v=float(env.reference_velocity),
+                n_obs=int(n), ox=ox, oy=oy, orad=r, sensors=np.array(env.sensor_data[:, 1], dtype=np.float64))
+
+
+def gen_path_rollouts(E, fname="path_traj.npz", per_k=6, T=100):
+    """Rollouts after reset(seed, options={'place_obstacles_on_path': k}) (simple_env.py:276-288),
+    k in {3, 8, 20, 35} (up to 29 + 35 = 64 obstacles): random-action steps (:310-346) with the
+    lidar over every obstacle (usv_asmc_ca_env.py:411-461), recorded up to each env's first episode
+    end (no autoreset: SB3 would reset without the option)."""
+    ks = (3, 8, 20, 35)
+    n_env = len(ks) * per_k
+    rng = np.random.default_rng(31)
+    acts = rng.uniform([0.2, -1], [1, 1], size=(n_env, T, 2)).astype(np.float32)
+    seeds = np.arange(n_env) + 700
+    kk = np.repeat(np.array(ks), per_k)
+    obs0 = np.zeros((n_env, 143), np.float32)
+    fobs = np.zeros((n_env, T, 143), np.float32)
+    rew = np.zeros((n_env, T))
+    term = np.zeros((n_env, T), bool)
+    trunc = np.zeros((n_env, T), bool)
+    steps = np.zeros(n_env, np.int64)
+    snaps = []
+    for e in range(n_env):
+        env = E.UsvSimpleEnv(render_mode=None)
+        obs0[e], _ = env.reset(seed=int(seeds[e]), options={"place_obstacles_on_path": int(kk[e])})
+        snaps.append(snapshot_full(env))
+        for t in range(T):
+            o, r, te, tr, _ = env.step(acts[e, t])
+            fobs[e, t], rew[e, t], term[e, t], trunc[e, t] = o, r, bool(te), bool(tr)
+            steps[e] = t + 1
+            if te or tr:
+                break
+    st = {f"init_{k}": np.stack([np.asarray(s[k]) for s in snaps]) for k in snaps[0]}
+    np.savez_compressed(os.path.join(HERE, fname), seeds=seeds, k=kk, actions=acts, obs0=obs0, final_obs=fobs,
+                        reward=rew, terminated=term, truncated=trunc, steps=steps, **st)
+    print(fname, "n_obs", st["init_n_obs"], "steps", steps)
+
+
 def main():
     refharness.load_reference()
     import gym_usv.envs as E
+    if "--r3" in sys.argv:              # round-3 fixtures only (existing files untouched)
+        gen_path_rollouts(E)
+        gen_info_traj(E, fname="asmc_info_traj.npz", cls=E.UsvSimpleASMCEnv, seed0=5100)
+        return
     if "--r2" in sys.argv:              # round-2 fixtures only (existing files untouched)
         gen_asmc_perturb(E)
         gen_info_traj(E)

@@ -333,7 +333,7 @@ def test_single_env_api():
 
 @pytest.mark.parametrize("env_id,precision", [("usv-simple", "f32"), ("usv-simple", "f64"),
                                               ("usv-asmc-simple", "f32")])
-def test_step_variants_bit_identical(env_id, precision, monkeypatch):
+def test_step_variants_bit_identical(env_id, precision):
     """Every step-kernel variant (envs/block, blind-sector skip, unroll, angular-window pair
     expansion) must give bit-identical outputs: pruning only removes pairs that cannot hit."""
     n, T = 2048, 24
@@ -343,8 +343,7 @@ def test_step_variants_bit_identical(env_id, precision, monkeypatch):
     ref = None
     for v in ("64,7,1", "32,0,1", "32,3,1", "16,7,1", "32,7,1", "16,0,2", "32,3,2", "8,7,2", "16,7,2", "32,7,2",
               "128,7,4", "128,7,5", "16,7,5"):
-        monkeypatch.setenv("USV_STEP_VARIANT", v)
-        env = make(env_id, n, seed=4, precision=precision)
+        env = make(env_id, n, seed=4, precision=precision, kernel_variant=v)
         env.reset(seed=4)
         outs = []
         for a in acts:
@@ -360,7 +359,7 @@ def test_step_variants_bit_identical(env_id, precision, monkeypatch):
 
 
 @pytest.mark.parametrize("n", [1, 77, 1077])
-def test_block_queue_ragged_sizes(n, monkeypatch):
+def test_block_queue_ragged_sizes(n):
     """Block-queue step (kinds 4, 5: 128-env blocks of 16 waves pulling env pairs from an LDS
     counter) on env counts that leave a partial block and an odd last pair: bit-identical to
     the fused wave kernel over a rollout with resets."""
@@ -370,8 +369,7 @@ def test_block_queue_ragged_sizes(n, monkeypatch):
             + torch.tensor([0.2, -1.0], device="cuda") for _ in range(T)]
     ref = None
     for v in ("64,7,1", "128,7,5", "16,7,5", "128,7,4", "16,7,2"):
-        monkeypatch.setenv("USV_STEP_VARIANT", v)
-        env = make("usv-simple", n, seed=6, max_episode_steps=12)
+        env = make("usv-simple", n, seed=6, max_episode_steps=12, kernel_variant=v)
         env.reset(seed=6)
         outs = []
         for a in acts:
@@ -387,7 +385,7 @@ def test_block_queue_ragged_sizes(n, monkeypatch):
 
 
 @pytest.mark.parametrize("precision", ["f32", "f64"])
-def test_step_variants_bit_identical_scattered(precision, monkeypatch):
+def test_step_variants_bit_identical_scattered(precision):
     """Variant bit-identity from injected poses spread over the field (far obstacles, envs
     near walls and corners), where the range-checked lidar paths run."""
     n = 4096
@@ -404,8 +402,7 @@ def test_step_variants_bit_identical_scattered(precision, monkeypatch):
     a = torch.from_numpy(rng.uniform([0.2, -1], [1, 1], size=(n, 2)).astype(np.float32)).cuda()
     ref = None
     for v in ("64,7,1", "32,3,1", "32,7,1", "16,0,1", "16,3,2", "8,7,2", "16,7,2", "128,7,4", "128,7,5", "16,7,5"):
-        monkeypatch.setenv("USV_STEP_VARIANT", v)
-        env = make("usv-simple", n, seed=3, precision=precision)
+        env = make("usv-simple", n, seed=3, precision=precision, kernel_variant=v)
         inject(env, orc.env, elapsed=1)
         o, r, te, tr, info = env.step(a)
         out = [x.clone() for x in (o, r, te, tr, info["final_obs"])]

@@ -99,14 +99,13 @@ def test_lidar_scenes_reset_scan(golden, precision):
     (None, "f32", "brute"),           # brute-force lidar (kind 1, lid 3)
     (None, "f64", "window"),          # f64 default (brute loop)
 ])
-def test_lidar_scenes_step(golden, variant, precision, lidar, monkeypatch):
+def test_lidar_scenes_step(golden, variant, precision, lidar):
     """The same scenes through the step kernels: zero velocity and zero action keep the pose
     bit-for-bit, so the step's obs row carries the scan of the fixture pose (reading / 100)."""
-    if variant:
-        monkeypatch.setenv("USV_STEP_VARIANT", variant)
     g = golden("lidar.npz")
     n = g["pos"].shape[0]
-    env = make("usv-simple", n, precision=precision, lidar=lidar, autoreset=False, max_episode_steps=0)
+    env = make("usv-simple", n, precision=precision, lidar=lidar, autoreset=False, max_episode_steps=0,
+               kernel_variant=variant)
     env.set_state(scene_state(g))
     obs, *_ = env.step(torch.zeros(n, 2, device="cuda"))
     (obs,) = to_np(obs)
@@ -228,10 +227,12 @@ def test_perturb_golden_replay(golden, precision):
         np.testing.assert_array_equal(trunc[m], g["truncated"][m, t], err_msg=f"t={t}")
         alive &= ~(g["terminated"][:, t] | g["truncated"][:, t])
     print(f"\n[perturb {precision}] max |hdr| err {hdr:.3e}, max |rew| err {rw:.3e}")
+    # f32: ~5x the r02 measurement (header 4.6e-6, reward 9.5e-5): a trajectory of 20 float32 ASMC
+    # substeps per step, the same bound as the plain usv-asmc-simple golden replay (test_gpu_parity)
     if precision == "f64":
         assert hdr <= 2e-6 and rw <= 1e-8
     else:
-        assert hdr <= 1e-3 and rw <= 1e-2
+        assert hdr <= 2.5e-5 and rw <= 5e-4
     env.close()
 
 
@@ -270,14 +271,17 @@ def test_step_info_matches_reference(golden, precision):
         assert info["left_thruster"].abs().max() == 0 and info["angle_action_reward"].abs().max() == 0
         for k in INFO_KEYS:
             v = info[k].detach().cpu().numpy().astype(np.float64)
-            worst[k] = max(worst.get(k, 0.0), float(np.abs(v[alive] - g["info_" + k][alive, t]).max()))
+            ref = g["info_" + k][alive, t]
+            worst[k] = max(worst.get(k, 0.0), float((np.abs(v[alive] - ref) / np.maximum(1.0, np.abs(ref))).max()))
         alive &= ~(g["terminated"][:, t] | g["truncated"][:, t])
         if not alive.any():
             break
     print(f"\n[info {precision}] " + ", ".join(f"{k} {v:.1e}" for k, v in worst.items()))
-    tol = 2e-6 if precision == "f64" else 2e-4        # f32 info values are float32 roundings
+    # errors relative to max(1, |value|) (position / path_end are ~100 m): f64 rows are float64 now;
+    # f32 ~5x the r02 measurement (ye_reward 1.2e-5, position 4.6e-6 m)
+    tol = 1e-10 if precision == "f64" else 6e-5
     for k, v in worst.items():
-        assert v <= tol * max(1.0, float(np.abs(g["info_" + k]).max())), (k, v)
+        assert v <= tol, (k, v)
     env.close()
 
 
@@ -364,13 +368,19 @@ def test_custom_experiment_numpy_exact(golden, precision):
     np.testing.assert_allclose(env.get_field("x"), g["init_position"][:, 0], atol=1e-6)
     np.testing.assert_allclose(env.get_field("path_x1"), g["init_path_end"][:, 0], atol=1e-5)
     alive = np.ones(n, bool)
+    he = re = 0.0
     for t in range(T):
         obs, rew, term, trunc, _ = env.step(torch.from_numpy(g["actions"][:, t]).cuda())
         obs, rew, term, trunc = to_np(obs, rew, term, trunc)
-        np.testing.assert_allclose(obs[alive, :15], g["final_obs"][alive, t, :15], rtol=1e-4,
-                                   atol=tol if precision == "f64" else 1e-4)
-        np.testing.assert_allclose(rew[alive], g["reward"][alive, t], atol=1e-8 if precision == "f64" else 1e-3)
+        # obs atol 1e-5 + rtol 1e-4, reward 1e-4 (f32); f64 to the float32 cast
+        np.testing.assert_allclose(obs[alive, :15], g["final_obs"][alive, t, :15], rtol=1e-4 if precision == "f32" else 0,
+                                   atol=tol if precision == "f64" else 1e-5)
+        np.testing.assert_allclose(rew[alive], g["reward"][alive, t], atol=1e-8 if precision == "f64" else 1e-4)
+        if alive.any():
+            he = max(he, float(np.abs(obs[alive, :15] - g["final_obs"][alive, t, :15]).max()))
+            re = max(re, float(np.abs(rew[alive] - g["reward"][alive, t]).max()))
         alive &= ~(term | trunc)
+    print(f"\n[experiment {precision}] header {he:.2e}, reward {re:.2e}")
     env.close()
 
 
@@ -396,11 +406,17 @@ def test_custom_experiment_autoreset_philox(golden):
     env.close()
 
 
-def test_constructor_options_validated():
-    with pytest.raises(ValueError):
-        make("usv-simple", 4, options={"no_such_option": 1})
-    with pytest.raises(ValueError):
-        make("usv-simple", 4).reset(options={"no_such_option": 1})
+def test_unknown_option_keys_ignored_like_the_reference():
+    """The reference reads only its known option keys and ignores the rest (simple_env.py:276, 292);
+    UsvSimpleASMCEnv.reset drops its options altogether (simple_env_asmc.py:14-16)."""
+    with pytest.warns(UserWarning):
+        env = make("usv-simple", 4, options={"no_such_option": 1})
+    env.reset(seed=0, options={"no_such_option": 1})              # ignored, as in the reference
+    env.close()
+    env = make("usv-asmc-simple", 4, obstacle_cap=32)
+    env.reset(seed=0, options={"place_obstacles_on_path": 8})     # dropped: no cap check applies
+    assert (env.get_field("n_obs") <= 29).all()
+    env.close()
 
 
 # --------------------------------------------------------------------------- sharding, two processes
@@ -449,28 +465,28 @@ def test_two_process_sharding_bit_identical():
 
 
 # --------------------------------------------------------------------------- vmcnt debug build
-@pytest.mark.parametrize("env_id,precision,variant", [
-    ("usv-simple", "f32", None),          # block-queue step (kind 5): LDS-DMA prefetch, vm_wait<7>
-    ("usv-asmc-simple", "f32", None),     # split block-queue step (kind 4)
-    ("usv-simple", "f32", "16,7,2"),      # split wave scan (kind 2): vm_wait<2|4>
-    ("usv-simple", "f64", None),          # fused wave kernel (kind 1)
+@pytest.mark.parametrize("env_id,precision,variant,n", [
+    ("usv-simple", "f32", None, 8192),        # small block-queue step (kind 5, 16 envs on 8 waves)
+    ("usv-simple", "f32", None, 65536),       # the headline 128-env / 16-wave block-queue step (kind 5)
+    ("usv-simple", "f32", "128,7,5", 8192),   # the same kernel forced at a small count (ragged tail too)
+    ("usv-asmc-simple", "f32", None, 8192),   # split block-queue step (kind 4)
+    ("usv-simple", "f32", "16,7,2", 8192),    # split wave scan (kind 2): vm_wait<2|4>
+    ("usv-simple", "f64", None, 8192),        # fused wave kernel (kind 1)
 ])
-def test_safe_vmcnt_build_bit_identical(env_id, precision, variant, monkeypatch):
+def test_safe_vmcnt_build_bit_identical(env_id, precision, variant, n):
     """libusvhip_safe.so (USV_SAFE_VMCNT: every hand-counted vm_wait is vmcnt(0)) against the product
     build over a rollout with resets: a miscounted wait in the product (a DMA'd obstacle row read
     before it landed) would make them differ."""
     from gym_usv_amd import _lib
     if not os.path.exists(_lib.SAFE_LIB_PATH):
         pytest.fail(f"{_lib.SAFE_LIB_PATH} not built (__graft_entry__.build() builds it)")
-    if variant:
-        monkeypatch.setenv("USV_STEP_VARIANT", variant)
-    n, T = 8192, 48
+    T = 48
     gen = torch.Generator(device="cuda").manual_seed(21)
     acts = [torch.rand(n, 2, device="cuda", generator=gen) * torch.tensor([0.8, 2.0], device="cuda")
             + torch.tensor([0.2, -1.0], device="cuda") for _ in range(T)]
     outs = []
     for path in (None, _lib.SAFE_LIB_PATH):
-        env = make(env_id, n, seed=13, precision=precision, max_episode_steps=20, lib_path=path)
+        env = make(env_id, n, seed=13, precision=precision, max_episode_steps=20, lib_path=path, kernel_variant=variant)
         env.reset(seed=13)
         seq = []
         for a in acts:

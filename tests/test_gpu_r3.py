@@ -1,0 +1,291 @@
+"""Round-3 GPU parity: the step path with more than 32 obstacles (reset option
+``place_obstacles_on_path``, up to 61 obstacle lanes, obstacle_cap 64), usv-asmc-simple's step info,
+f64 info rows, and the gymnasium ``copy`` semantics of the vector env.  Run on an MI355X: pytest -m gpu.
+
+Fixtures come from the reference itself (tests/golden/make_golden.py ``--r3``).  Tolerances are
+SURVEY.md §8(c)'s: fp32 kernel vs the float64 reference obs atol 1e-5 + rtol 1e-4, reward atol 1e-4,
+lidar rays that flip hit/miss at a grazing edge <= 1e-4 of rays; float64 kernel: obs equal after the
+float32 cast (at most a last-bit flip of the cast), reward 1e-9.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import usv_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+F32_OBS_ATOL, F32_OBS_RTOL, F32_REW_ATOL = 1e-5, 1e-4, 1e-4
+
+
+def make(env_id, n, **kw):
+    import gym_usv_amd
+    return gym_usv_amd.make_vec(env_id, n, device=0, **kw)
+
+
+def to_np(*ts):
+    torch.cuda.synchronize()
+    return [t.detach().cpu().numpy() for t in ts]
+
+
+def f32_ulp(x):
+    return np.spacing(np.abs(x).astype(np.float32)).astype(np.float64)
+
+
+# --------------------------------------------------------------------------- > 32 obstacles
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_path_obstacle_rollouts_numpy_exact(golden, precision):
+    """Reference rollouts after reset(seed, options={'place_obstacles_on_path': k}), k in {3, 8, 20,
+    35} (simple_env.py:276-288, 310-346): NumPy-exact resets with obstacle_cap 64, then the
+    reference's random actions, every step compared up to each env's first episode end.  k = 20, 35
+    put 33-64 obstacles in an env, so the step runs the > 32-obstacle lidar (one env per wave)."""
+    g = golden("path_traj.npz")
+    T = g["actions"].shape[1]
+    worst = {"obs0": 0.0, "hdr": 0.0, "sens": 0.0, "rew": 0.0}
+    flips = rays = coll = steps = 0
+    for k in np.unique(g["k"]):
+        idx = np.flatnonzero(g["k"] == k)
+        env = make("usv-simple", len(idx), precision=precision, autoreset=False, reset_rng="numpy",
+                   obstacle_cap=64)
+        obs, _ = env.reset(seed=[int(s) for s in g["seeds"][idx]], options={"place_obstacles_on_path": int(k)})
+        (obs,) = to_np(obs)
+        np.testing.assert_array_equal(env.get_field("n_obs"), g["init_n_obs"][idx])
+        worst["obs0"] = max(worst["obs0"], float(np.abs(obs - g["obs0"][idx]).max()))
+        alive = np.ones(len(idx), bool)
+        for t in range(T):
+            obs, rew, term, trunc, _ = env.step(torch.from_numpy(g["actions"][idx, t]).cuda())
+            obs, rew, term, trunc = to_np(obs, rew, term, trunc)
+            m = alive
+            if not m.any():
+                break
+            ref = g["final_obs"][idx][m, t]
+            np.testing.assert_array_equal(term[m], g["terminated"][idx][m, t], err_msg=f"k={k} t={t}")
+            np.testing.assert_array_equal(trunc[m], g["truncated"][idx][m, t], err_msg=f"k={k} t={t}")
+            he = np.abs(obs[m, :15] - ref[:, :15])
+            se = np.abs(obs[m, 15:] - ref[:, 15:])
+            re = np.abs(rew[m] - g["reward"][idx][m, t])
+            if precision == "f64":
+                # the same float64 values cast to float32: equal, or one last-bit flip of the cast
+                assert (he <= f32_ulp(ref[:, :15])).all() and (se <= f32_ulp(ref[:, 15:])).all(), (k, t)
+                worst["hdr"] = max(worst["hdr"], float(he.max()))
+                worst["sens"] = max(worst["sens"], float(se.max()))
+                worst["rew"] = max(worst["rew"], float(re.max()))
+            else:
+                assert (he <= F32_OBS_ATOL + F32_OBS_RTOL * np.abs(ref[:, :15])).all(), (k, t, he.max())
+                bad = se > F32_OBS_ATOL + F32_OBS_RTOL * np.abs(ref[:, 15:])
+                flips += int(bad.sum())
+                worst["hdr"] = max(worst["hdr"], float(he.max()))
+                worst["sens"] = max(worst["sens"], float(se[~bad].max(initial=0.0)))
+                c = np.abs(re - 20) < 1                  # min sensor within rounding of 0.2 (:153-156)
+                coll += int(c.sum())
+                worst["rew"] = max(worst["rew"], float(re[~c].max(initial=0.0)))
+            rays += int(m.sum()) * 128
+            steps += int(m.sum())
+            alive &= ~(g["terminated"][idx][:, t] | g["truncated"][idx][:, t])
+        env.close()
+    print(f"\n[path rollouts {precision}] {steps} env-steps: reset obs {worst['obs0']:.2e}, header "
+          f"{worst['hdr']:.2e}, sensors {worst['sens']:.2e}, reward {worst['rew']:.2e}, grazing flips "
+          f"{flips}/{rays}, collision-threshold flips {coll}")
+    assert steps >= 1000 and g["init_n_obs"].max() > 60
+    if precision == "f64":
+        assert worst["obs0"] <= 6e-8 and worst["rew"] <= 1e-9
+    else:
+        assert worst["obs0"] <= 2e-5 and worst["rew"] <= F32_REW_ATOL
+        assert flips <= max(2, rays // 10000) and coll <= 1
+
+
+def _many_obstacle_oracle(n, k, seed, cap=64):
+    """n oracle envs with `k` path obstacles each (33..61 obstacles at k = 32) at scattered poses."""
+    e = O.SimpleEnvBatch(n, cap=cap)
+    e.reset(seeds=list(range(seed, seed + n)), options={"place_obstacles_on_path": k})
+    rng = np.random.default_rng(seed)
+    for _ in range(3):
+        e.step(rng.uniform([0.2, -1], [1, 1], size=(n, 2)))
+    # poses over the field (a quarter far out, so the lidar's max-range test matters), some inside
+    # an obstacle
+    xy = rng.uniform(0.3, 25, size=(n, 2))
+    q = n // 4
+    xy[:q] = rng.uniform(60, 99, size=(q, 2))
+    ins = rng.random(n) < 0.05
+    xy[ins, 0], xy[ins, 1] = e.ox[ins, 0] + 0.05, e.oy[ins, 0]
+    e.position[:, :2] = xy
+    e.position[:, 2] = rng.uniform(-6, 6, n)
+    return e, rng
+
+
+def _inject(env, e):
+    env.set_state(e.get_state())
+    env.set_field("elapsed", 1)
+    env.set_field("scan_valid", 1)
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_many_obstacles_single_step_parity(precision):
+    """One step from oracle states with 33-61 obstacles per env (cap 64) vs the oracle, scattered
+    poses (far obstacles, boats inside obstacles): the > 32-obstacle step path at scale."""
+    n = 2048
+    e, rng = _many_obstacle_oracle(n, 32, 500)
+    assert e.n_obs.min() > 32
+    env = make("usv-simple", n, precision=precision, autoreset=False, obstacle_cap=64, max_episode_steps=0)
+    _inject(env, e)
+    a = rng.uniform([0.2, -1], [1, 1], size=(n, 2)).astype(np.float32)
+    obs, rew, term, trunc, _ = env.step(torch.from_numpy(a).cuda())
+    g_obs, g_rew, g_term, g_trunc = to_np(obs, rew, term, trunc)
+    o_obs, o_rew, o_term, o_trunc = e.step(a)
+    ok = (g_term == o_term) & (g_trunc == o_trunc)
+    assert (~ok).sum() <= (0 if precision == "f64" else 1)
+    he = np.abs(g_obs[ok, :15] - o_obs[ok, :15])
+    se = np.abs(g_obs[ok, 15:] - o_obs[ok, 15:])
+    re = np.abs(g_rew[ok] - o_rew[ok])
+    if precision == "f64":
+        assert (he <= f32_ulp(o_obs[ok, :15])).all() and (se <= f32_ulp(o_obs[ok, 15:])).all()
+        assert re.max() <= 1e-9
+        print(f"\n[cap64 f64] header {he.max():.2e}, sensors {se.max():.2e}, reward {re.max():.2e}")
+    else:
+        assert (he <= F32_OBS_ATOL + F32_OBS_RTOL * np.abs(o_obs[ok, :15])).all(), he.max()
+        bad = se > F32_OBS_ATOL + F32_OBS_RTOL * np.abs(o_obs[ok, 15:])
+        c = np.abs(re - 20) < 1
+        print(f"\n[cap64 f32] header {he.max():.2e}, reward {re[~c].max():.2e}, grazing flips "
+              f"{int(bad.sum())}/{bad.size}, collision flips {int(c.sum())}")
+        assert bad.mean() <= 1e-4 and re[~c].max() <= F32_REW_ATOL and c.sum() <= 1
+
+
+@pytest.mark.parametrize("precision", ["f32", "f64"])
+def test_many_obstacles_variants_bit_identical(precision):
+    """Every step-kernel variant that runs cap > 32 (fused wave kernel, split wave scan; brute and
+    blind-sector brute and angular-window lidar; 16-64 envs per block) gives bit-identical outputs
+    with 33-61 obstacles per env, over a 24-step rollout with same-step autoresets (TimeLimit 8)."""
+    n, T = 2048, 24
+    e, rng = _many_obstacle_oracle(n, 32, 900)
+    acts = [torch.from_numpy(rng.uniform([0.2, -1], [1, 1], size=(n, 2)).astype(np.float32)).cuda()
+            for _ in range(T)]
+    ref = None
+    for v in ("64,7,1", "16,7,1", "32,3,1", "16,0,1", "16,7,2", "8,3,2", "32,0,2"):
+        env = make("usv-simple", n, seed=8, precision=precision, obstacle_cap=64, max_episode_steps=8,
+                   kernel_variant=v)
+        _inject(env, e)
+        outs = []
+        for a in acts:
+            o, r, te, tr, info = env.step(a)
+            outs.append((o, r, te, tr, info["final_obs"], info["_final_obs"]))
+        env.close()
+        if ref is None:
+            ref = outs
+            continue
+        for t, (x, y) in enumerate(zip(ref, outs)):
+            m = x[5]
+            for u, w in zip(x[:4], y[:4]):
+                assert torch.equal(u, w), f"variant {v} differs at step {t}"
+            assert torch.equal(x[4][m], y[4][m]), f"variant {v}: final_obs differs at step {t}"
+
+
+def test_kernel_variant_validation():
+    """usv_set_kernel_variant refuses what the config cannot run (the block queue needs f32 and
+    cap <= 32) and unknown shapes."""
+    import gym_usv_amd
+    with pytest.raises(gym_usv_amd.UsvLibError):
+        make("usv-simple", 64, obstacle_cap=64, kernel_variant="128,7,5")
+    with pytest.raises(gym_usv_amd.UsvLibError):
+        make("usv-simple", 64, precision="f64", kernel_variant="128,7,4")
+    with pytest.raises(gym_usv_amd.UsvLibError):
+        make("usv-simple", 64, kernel_variant="48,7,1")
+    with pytest.raises(gym_usv_amd.UsvLibError):
+        make("usv-asmc-v0", 64, kernel_variant="64,7,1")
+
+
+# --------------------------------------------------------------------------- info
+INFO_KEYS = ("position", "velocity", "path_start", "path_end", "reward", "action0", "action1", "ye",
+             "angle_to_target", "ye_reward", "angle_to_target_reward", "delta_action_reward", "delta_action",
+             "velocity_track_reward", "reference_velocity", "reward_velocity", "reference_velocity_error")
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_asmc_simple_step_info_matches_reference(golden, precision):
+    """usv-asmc-simple's step info is UsvSimpleEnv.step's after the two ASMC computes
+    (simple_env_asmc.py:18-27, simple_env.py:102-115, 189-199): every key, from the reference's
+    NumPy-exact resets, up to each env's first episode end.  In the f64 build the info rows are
+    float64 like the reference's values."""
+    g = golden("asmc_info_traj.npz")
+    n, T = g["actions"].shape[:2]
+    env = make("usv-asmc-simple", n, precision=precision, autoreset=False, info=True, reset_rng="numpy")
+    obs, info = env.reset(seed=[int(s) for s in g["seeds"]])
+    want = torch.float64 if precision == "f64" else torch.float32
+    assert info["position"].dtype == want and info["reward"].dtype == want
+    for k in ("position", "velocity", "path_start", "path_end", "reward", "ye", "angle_to_target"):
+        v = info[k].detach().cpu().numpy().astype(np.float64)
+        np.testing.assert_allclose(v, g["info0_" + k], rtol=0, atol=1e-12 if precision == "f64" else 2e-5 * max(
+            1.0, float(np.abs(g["info0_" + k]).max())), err_msg=k)
+    alive = np.ones(n, bool)
+    worst = {}
+    for t in range(T):
+        obs, rew, term, trunc, info = env.step(torch.from_numpy(g["actions"][:, t]).cuda())
+        torch.cuda.synchronize()
+        for k in INFO_KEYS:
+            v = info[k].detach().cpu().numpy().astype(np.float64)
+            ref = g["info_" + k][alive, t]
+            err = np.abs(v[alive] - ref)
+            # relative to the key's magnitude (position, path_end ~ 100 m)
+            worst[k] = max(worst.get(k, 0.0), float((err / np.maximum(1.0, np.abs(ref))).max()))
+        alive &= ~(g["terminated"][:, t] | g["truncated"][:, t])
+        if not alive.any():
+            break
+    print(f"\n[asmc info {precision}] " + ", ".join(f"{k} {v:.1e}" for k, v in worst.items()))
+    # f64: the reference's float64 arithmetic order (ASMC bit-exact); f32: 20 float32 ASMC substeps
+    tol = 1e-9 if precision == "f64" else 1e-4
+    for k, v in worst.items():
+        assert v <= tol, (k, v)
+    env.close()
+
+
+def test_f64_info_rows_match_reference_path_end(golden):
+    """Round 2 kept f64 info rows in float32 (path_end off by 3.4e-6); they are float64 now."""
+    g = golden("simple_info_traj.npz")
+    n = g["seeds"].shape[0]
+    env = make("usv-simple", n, precision="f64", autoreset=False, info=True, reset_rng="numpy")
+    _, info = env.reset(seed=[int(s) for s in g["seeds"]])
+    np.testing.assert_allclose(info["path_end"].cpu().numpy(), g["info0_path_end"], rtol=0, atol=1e-12)
+    _, _, _, _, info = env.step(torch.from_numpy(g["actions"][:, 0]).cuda())
+    np.testing.assert_allclose(info["path_end"].cpu().numpy(), g["info_path_end"][:, 0], rtol=0, atol=1e-12)
+    np.testing.assert_allclose(info["position"].cpu().numpy(), g["info_position"][:, 0], rtol=0, atol=1e-12)
+    env.close()
+
+
+# --------------------------------------------------------------------------- copy semantics
+def test_copy_semantics():
+    """copy=True (default, gymnasium SyncVectorEnv's convention): each step returns tensors of its
+    own, so kept outputs are not overwritten; copy=False returns the persistent buffers.  Both give
+    the same values."""
+    n, T = 256, 6
+    gen = torch.Generator(device="cuda").manual_seed(2)
+    acts = [torch.rand(n, 2, device="cuda", generator=gen) for _ in range(T)]
+    a = make("usv-simple", n, seed=5, max_episode_steps=3)
+    b = make("usv-simple", n, seed=5, max_episode_steps=3, copy=False)
+    oa, _ = a.reset(seed=5)
+    ob, _ = b.reset(seed=5)
+    assert torch.equal(oa, ob)
+    kept_a, kept_b = [], []
+    for x in acts:
+        ra = a.step(x)
+        rb = b.step(x)
+        for u, w in zip(ra[:4], rb[:4]):
+            assert torch.equal(u, w)
+        kept_a.append(ra)
+        kept_b.append(rb)
+    assert len({r[0].data_ptr() for r in kept_a}) == T          # fresh obs every step
+    assert len({r[0].data_ptr() for r in kept_b}) == 1          # the persistent buffer
+    # the kept copy=True outputs are still the values of their own step
+    c = make("usv-simple", n, seed=5, max_episode_steps=3, copy=False)
+    c.reset(seed=5)
+    for x, r in zip(acts, kept_a):
+        o, rew, te, tr, info = c.step(x)
+        assert torch.equal(o, r[0]) and torch.equal(rew, r[1]) and torch.equal(te, r[2]) and torch.equal(tr, r[3])
+        m = info["_final_obs"]
+        assert torch.equal(m, r[4]["_final_obs"]) and torch.equal(info["final_obs"][m], r[4]["final_obs"][m])
+    # a masked reset keeps the other rows of the latest obs
+    mask = torch.zeros(n, dtype=torch.bool, device="cuda")
+    mask[:7] = True
+    last = kept_a[-1][0]
+    o2, _ = a.reset(mask=mask)
+    assert torch.equal(o2[7:], last[7:]) and o2.data_ptr() != last.data_ptr()
+    for e in (a, b, c):
+        e.close()

@@ -215,3 +215,51 @@ def test_custom_experiment_matches_reference(golden):
         np.testing.assert_allclose(o[alive], g["final_obs"][alive, t], rtol=1e-6, atol=1e-6)
         np.testing.assert_allclose(r[alive], g["reward"][alive, t], rtol=1e-9, atol=1e-9)
         alive &= ~(te | tr)
+
+
+# --------------------------------------------------------------------------- round-3 fixtures
+def test_place_obstacles_on_path_rollouts_match_reference(golden):
+    """Rollouts after reset(seed, options={'place_obstacles_on_path': k}) (simple_env.py:276-288,
+    310-346), k up to 35 (61 obstacles): the lidar over every obstacle (usv_asmc_ca_env.py:411-461)."""
+    g = golden("path_traj.npz")
+    n, T = g["actions"].shape[:2]
+    assert g["init_n_obs"].max() > 32           # the > 32-obstacle path is what this pins
+    for k in np.unique(g["k"]):
+        idx = np.flatnonzero(g["k"] == k)
+        e = O.SimpleEnvBatch(len(idx), cap=64)
+        obs = e.reset(seeds=[int(s) for s in g["seeds"][idx]], options={"place_obstacles_on_path": int(k)})
+        np.testing.assert_allclose(obs, g["obs0"][idx], rtol=1e-6, atol=1e-6)
+        np.testing.assert_array_equal(e.n_obs, g["init_n_obs"][idx])
+        np.testing.assert_allclose(e.ox, g["init_ox"][idx], atol=1e-12)
+        alive = np.ones(len(idx), bool)
+        for t in range(T):
+            o, r, te, tr = e.step(g["actions"][idx, t])
+            m = alive
+            np.testing.assert_array_equal(te[m], g["terminated"][idx][m, t], err_msg=f"k={k} t={t}")
+            np.testing.assert_array_equal(tr[m], g["truncated"][idx][m, t], err_msg=f"k={k} t={t}")
+            np.testing.assert_allclose(o[m], g["final_obs"][idx][m, t], rtol=1e-6, atol=1e-6, err_msg=f"k={k} t={t}")
+            np.testing.assert_allclose(r[m], g["reward"][idx][m, t], rtol=1e-9, atol=1e-9, err_msg=f"k={k} t={t}")
+            alive &= ~(g["terminated"][idx][:, t] | g["truncated"][idx][:, t])
+            if not alive.any():
+                break
+
+
+def test_asmc_simple_step_info_matches_reference(golden):
+    """usv-asmc-simple's step info: UsvSimpleEnv.step's info after the two ASMC computes
+    (simple_env_asmc.py:18-27, simple_env.py:102-115, 189-199)."""
+    g = golden("asmc_info_traj.npz")
+    n, T = g["actions"].shape[:2]
+    e = O.SimpleAsmcEnvBatch(n)
+    e.reset(seeds=[int(s) for s in g["seeds"]])
+    inf = e.reset_info()
+    for k in ("position", "velocity", "path_start", "path_end", "reward", "ye", "angle_to_target"):
+        np.testing.assert_allclose(inf[k], g["info0_" + k], rtol=1e-12, atol=1e-12, err_msg=k)
+    alive = np.ones(n, bool)
+    for t in range(T):
+        e.step(g["actions"][:, t])
+        for k, v in e.info.items():
+            np.testing.assert_allclose(v[alive], g["info_" + k][alive, t], rtol=1e-8, atol=1e-8,
+                                       err_msg=f"{k} t={t}")
+        alive &= ~(g["terminated"][:, t] | g["truncated"][:, t])
+        if not alive.any():
+            break
