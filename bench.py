@@ -10,10 +10,18 @@ region (inputs resident in HBM).  Multi-GPU: one process per GPU, envs sharded b
 (env_id_offset = rank * N), no collective on the step path (weak scaling); the only
 collectives are the barrier and the max-over-ranks of the elapsed time.
 
+Warm-up: the W warm-up steps, then more untimed steps until --clock-warmup seconds have passed
+(the GPU clock ramps over the first few hundred milliseconds of work; a short --warmup would
+otherwise time a cold chip).  The line reports both counts.
+
 Rank 0 prints one JSON line: value = all ranks' env-steps / max-rank time, plus
   roofline:     algorithmic bytes per launch / mean launch duration (HIP events around groups of
                 back-to-back launches on the env's stream) vs 8 TB/s; traffic from the committed
-                rocprofv3 PMC summary (profiles/pmc_summary.json) when it matches the workload.
+                rocprofv3 PMC summary (profiles/pmc_summary.json) when it matches the workload;
+                valu_frac = VALU wave-instructions per launch (same summary, SQ_INSTS_VALU) x 2
+                cycles (a wave64 VALU instruction on a SIMD-32) / (1024 SIMDs x 2.4 GHz x launch time).
+  api_step:     the public UsvVectorEnv.step() (ctypes call, checks, output tensors) timed over the
+                same envs, copy=True (fresh output tensors) and copy=False (persistent buffers).
   cpu_baseline: the CPU oracle (per-env NumPy restatement of the reference step, oracle/) timed
                 on this host's cores for a bounded sample.
 """
@@ -33,6 +41,7 @@ for _p in (ROOT, os.path.join(ROOT, "gym-usv_amd")):
         sys.path.insert(0, _p)
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip-level table)
+SIMDS, CLOCK_GHZ, VALU_CYCLES = 1024, 2.4, 2   # 256 CUs x 4 SIMD-32; max clock; wave64 VALU issue
 METRIC = "env-steps/sec at 65 536 parallel envs; 1/2/4/8 MI355X scaling"
 
 
@@ -187,6 +196,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--event-every", type=int, default=16, help="launches per HIP-event-timed group")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_summary.json"))
+    ap.add_argument("--clock-warmup", type=float, default=0.3,
+                    help="untimed steps after --warmup until this many seconds have passed")
+    ap.add_argument("--api-steps", type=int, default=200, help="steps of the public-API leg (0 = skip)")
+    ap.add_argument("--variant", default=None, help="step-kernel variant epb,lid,kind (tools; default: tuned)")
     args = ap.parse_args()
 
     import torch
@@ -204,7 +217,7 @@ def main():
     import gym_usv_amd
     N, K, W = args.envs, args.steps, args.warmup
     env = gym_usv_amd.make_vec(args.env_id, N, device=local, seed=args.seed, precision=args.precision,
-                               lidar=args.lidar, env_id_offset=shard(rank, N)[0])
+                               lidar=args.lidar, env_id_offset=shard(rank, N)[0], kernel_variant=args.variant)
     env.reset(seed=args.seed)
     mean_obs = float(env.get_field("n_obs").mean())
     A, D = env.act_dim, env.obs_dim
@@ -232,6 +245,15 @@ def main():
 
     for k in range(W):
         launch(k)
+    # clock warm-up (untimed): keep stepping until the GPU has been busy for --clock-warmup seconds
+    torch.cuda.synchronize(dev)
+    extra, tw = 0, time.perf_counter()
+    while time.perf_counter() - tw < args.clock_warmup:
+        for _ in range(64):
+            launch(W + extra)
+            extra += 1
+        torch.cuda.synchronize(dev)
+    W2 = W + extra
     # HIP events on the env's stream bracket groups of G back-to-back launches (one event pair
     # per group; a pair around every single launch would add its own gap to each launch)
     G = max(1, args.event_every)
@@ -246,7 +268,7 @@ def main():
         g, r = divmod(k, G)
         if g < groups and r == 0:
             ev[g][0].record(stream)
-        launch(W + k)
+        launch(W2 + k)
         if g < groups and r == G - 1:
             ev[g][1].record(stream)
     torch.cuda.synchronize(dev)
@@ -257,23 +279,47 @@ def main():
     kern_ms = (sum(a.elapsed_time(b) for a, b in ev) / (groups * G)) if groups else elapsed / K * 1e3
     elapsed, kern_ms = reduce_max([elapsed, kern_ms], device=dev)
 
+    # public API leg (untimed by the contract above): UsvVectorEnv.step on the same envs
+    api = None
+    if args.api_steps > 0:
+        api = {}
+        for copy in (True, False):
+            env.copy = copy
+            for k in range(8):
+                env.step(acts[k % pool])
+            torch.cuda.synchronize(dev)
+            t1 = time.perf_counter()
+            for k in range(args.api_steps):
+                env.step(acts[k % pool])
+            torch.cuda.synchronize(dev)
+            dt = (time.perf_counter() - t1) / args.api_steps
+            api["copy" if copy else "nocopy"] = {"env_steps_per_s": round(N / dt, 1), "us_per_step": round(dt * 1e6, 2)}
+        api["steps"] = args.api_steps
+        api["note"] = ("UsvVectorEnv.step(actions) -> (obs, reward, terminated, truncated, info) with torch "
+                       "tensors on the device; copy=True returns fresh tensors (gymnasium default), copy=False "
+                       "the persistent buffers")
+
     if rank == 0:
         value = aggregate_rate(N, world, K, elapsed)
         bpe = algorithmic_bytes_per_env_step(args.env_id, mean_obs, args.precision)
         bytes_per_launch = bpe * N
         achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
-        traffic = None
+        traffic = valu = None
         if os.path.exists(args.pmc):
             try:
                 pmc = json.load(open(args.pmc))
                 key = f"{args.env_id}/{N}/{args.precision}/{args.lidar}"
                 if key in pmc:
                     traffic = pmc[key]["hbm_bytes_per_launch"]
+                    valu = pmc[key].get("sq_insts_valu_per_launch")
             except Exception:
-                traffic = None
+                traffic = valu = None
+        valu_frac = None
+        if valu:
+            valu_frac = round(valu * VALU_CYCLES / (SIMDS * CLOCK_GHZ * 1e9 * kern_ms * 1e-3), 4)
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world,
-            "steps": K, "warmup": W, "ms_per_step": round(elapsed / K * 1e3, 5),
+            "steps": K, "warmup": W, "clock_warmup_steps": extra, "ms_per_step": round(elapsed / K * 1e3, 5),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": args.precision, "data": "synthetic (on-device uniform random actions, Philox env resets)",
             "config": {"workload": f"C3: {args.env_id}, {N} envs per GPU, random-action rollout, "
@@ -284,7 +330,11 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "kernel_ms": round(kern_ms, 5),
-                         "algorithmic_bytes_per_env_step": round(bpe, 1)},
+                         "algorithmic_bytes_per_env_step": round(bpe, 1),
+                         "valu_frac": valu_frac,
+                         "valu_basis": "SQ_INSTS_VALU per launch (profiles/pmc_summary.json) x 2 cycles / "
+                                       "(1024 SIMDs x 2.4 GHz x kernel_ms)" if valu_frac is not None else None},
+            "api_step": api,
         }
         if args.env_id in LEGACY_IDS:
             out["config"].pop("lidar")

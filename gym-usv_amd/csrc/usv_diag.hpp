@@ -7,7 +7,7 @@
 #error "usv_diag.hpp is for the diagnostic builds only (-DUSV_DIAG)"
 #endif
 
-namespace usv {
+// (included inside namespace usv by usv_kernels.hip)
 
 // Diagnostic build only (-DUSV_DIAG_STAMPS): per-block s_memrealtime (100 MHz) stamps at the
 // phase boundaries of the step kernel, read back with usv_diag_stamps().  Never in the product.
@@ -107,5 +107,3 @@ struct QProf { __device__ void mark(int) {} __device__ void count(int, unsigned 
 #define QCOUNT(i, k) do {} while (0)
 __device__ __forceinline__ void qprof_flush(QProf*) {}
 #endif
-
-}  // namespace usv

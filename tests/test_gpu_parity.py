@@ -341,8 +341,8 @@ def test_step_variants_bit_identical(env_id, precision):
     acts = [torch.rand(n, 2, device="cuda", generator=gen) * torch.tensor([0.8, 2.0], device="cuda")
             + torch.tensor([0.2, -1.0], device="cuda") for _ in range(T)]
     ref = None
-    for v in ("64,7,1", "32,0,1", "32,3,1", "16,7,1", "32,7,1", "16,0,2", "32,3,2", "8,7,2", "16,7,2", "32,7,2",
-              "128,7,4", "128,7,5", "16,7,5"):
+    queue = ("128,7,4", "128,7,5", "16,7,5") if precision == "f32" else ()   # block queue: f32 only
+    for v in ("64,7,1", "32,0,1", "32,3,1", "16,7,1", "32,7,1", "16,0,2", "32,3,2", "8,7,2", "16,7,2", "32,7,2") + queue:
         env = make(env_id, n, seed=4, precision=precision, kernel_variant=v)
         env.reset(seed=4)
         outs = []
@@ -369,7 +369,7 @@ def test_block_queue_ragged_sizes(n):
             + torch.tensor([0.2, -1.0], device="cuda") for _ in range(T)]
     ref = None
     for v in ("64,7,1", "128,7,5", "16,7,5", "128,7,4", "16,7,2"):
-        env = make("usv-simple", n, seed=6, max_episode_steps=12, kernel_variant=v)
+        env = make("usv-simple", n, seed=6, max_episode_steps=12, kernel_variant=v, copy=False)
         env.reset(seed=6)
         outs = []
         for a in acts:
@@ -401,8 +401,10 @@ def test_step_variants_bit_identical_scattered(precision):
     assert far.mean() > 0.1, far.mean()          # the far path is actually exercised
     a = torch.from_numpy(rng.uniform([0.2, -1], [1, 1], size=(n, 2)).astype(np.float32)).cuda()
     ref = None
-    for v in ("64,7,1", "32,3,1", "32,7,1", "16,0,1", "16,3,2", "8,7,2", "16,7,2", "128,7,4", "128,7,5", "16,7,5"):
-        env = make("usv-simple", n, seed=3, precision=precision, kernel_variant=v)
+    queue = ("128,7,4", "128,7,5", "16,7,5") if precision == "f32" else ()   # block queue: f32 only
+    for v in ("64,7,1", "32,3,1", "32,7,1", "16,0,1", "16,3,2", "8,7,2", "16,7,2") + queue:
+        # copy=False: final_obs rows of envs that did not end keep the (identical) buffer contents
+        env = make("usv-simple", n, seed=3, precision=precision, kernel_variant=v, copy=False)
         inject(env, orc.env, elapsed=1)
         o, r, te, tr, info = env.step(a)
         out = [x.clone() for x in (o, r, te, tr, info["final_obs"])]

@@ -424,7 +424,8 @@ def _shard_worker(rank, world, tmp, n, steps):
     import torch.distributed as dist
     dist.init_process_group("gloo", init_method=f"file://{tmp}/store", rank=rank, world_size=world)
     import gym_usv_amd
-    env = gym_usv_amd.make_vec("usv-simple", n, device=0, seed=21, env_id_offset=rank * n, max_episode_steps=30)
+    env = gym_usv_amd.make_vec("usv-simple", n, device=0, seed=21, env_id_offset=rank * n, max_episode_steps=30,
+                               copy=False)
     env.reset(seed=21)
     gen = torch.Generator().manual_seed(99)
     outs = []
@@ -448,7 +449,7 @@ def test_two_process_sharding_bit_identical():
     with tempfile.TemporaryDirectory() as tmp:
         mp.start_processes(_shard_worker, args=(world, tmp, n, steps), nprocs=world, join=True, start_method="spawn")
         parts = [torch.load(os.path.join(tmp, f"rank{r}.pt"), weights_only=True) for r in range(world)]
-    env = make("usv-simple", world * n, seed=21, max_episode_steps=30)
+    env = make("usv-simple", world * n, seed=21, max_episode_steps=30, copy=False)
     env.reset(seed=21)
     gen = torch.Generator().manual_seed(99)
     for t in range(steps):
@@ -486,7 +487,8 @@ def test_safe_vmcnt_build_bit_identical(env_id, precision, variant, n):
             + torch.tensor([0.2, -1.0], device="cuda") for _ in range(T)]
     outs = []
     for path in (None, _lib.SAFE_LIB_PATH):
-        env = make(env_id, n, seed=13, precision=precision, max_episode_steps=20, lib_path=path, kernel_variant=variant)
+        env = make(env_id, n, seed=13, precision=precision, max_episode_steps=20, lib_path=path, kernel_variant=variant,
+                   copy=False)
         env.reset(seed=13)
         seq = []
         for a in acts:

@@ -231,7 +231,9 @@ def test_asmc_simple_step_info_matches_reference(golden, precision):
             break
     print(f"\n[asmc info {precision}] " + ", ".join(f"{k} {v:.1e}" for k, v in worst.items()))
     # f64: the reference's float64 arithmetic order (ASMC bit-exact); f32: 20 float32 ASMC substeps
-    tol = 1e-9 if precision == "f64" else 1e-4
+    # per step accumulate position rounding (ye_reward's slope is 1/0.075 per metre): the trajectory
+    # bound of the usv-asmc-simple golden replay (test_gpu_parity.py)
+    tol = 1e-9 if precision == "f64" else 5e-4
     for k, v in worst.items():
         assert v <= tol, (k, v)
     env.close()

@@ -1,11 +1,13 @@
-# Diagnostic builds of the step library (never the product): ablations and per-wave stamps.
-#   bash tools/build_diag.sh NOLIDAR NOSTORE NODYN STAMPS ...   -> diag/abl_<X>.so / diag/stamps.so
+# Diagnostic builds of the step library (never the product): clock stamps / section counters.
+#   bash tools/build_diag.sh STAMPS QPROF PROF   -> diag/stamps.so, diag/qprof.so, diag/prof.so
+# Each defines USV_DIAG (csrc/usv_diag.hpp is included only then) plus USV_DIAG_<X>.
 set -e
 cd "$(dirname "$0")/.."
 mkdir -p diag
 for x in "$@"; do
-  if [ "$x" = STAMPS ]; then def=-DUSV_DIAG_STAMPS; out=diag/stamps.so; else def=-DUSV_ABL_$x; out=diag/abl_$x.so; fi
-  /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -fPIC -shared -mllvm -amdgpu-atomic-optimizer-strategy=None -Iinclude $def -o $out gym-usv_amd/csrc/usv_kernels.hip &
+  lc=$(echo $x | tr A-Z a-z)
+  /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 -std=c++17 -fPIC -shared -mllvm -amdgpu-atomic-optimizer-strategy=None \
+    -Iinclude -DUSV_DIAG -DUSV_DIAG_$x -o diag/$lc.so gym-usv_amd/csrc/usv_kernels.hip &
 done
 wait
 ls -la diag

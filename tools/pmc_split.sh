@@ -1,10 +1,10 @@
-# kernel trace + VALU/LDS/wait counters for one step variant (USV_STEP_VARIANT)
+# kernel trace + VALU/LDS/wait counters for one step variant: bash tools/pmc_split.sh TAG [epb,lid,kind]
 set -e
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 O=gpurun_out/pmc_${1:-x}
 mkdir -p $O
-B="python3 bench.py --steps 40 --warmup 5 --no-cpu-baseline"
+B="python3 bench.py --steps 40 --warmup 5 --clock-warmup 0 --api-steps 0 --no-cpu-baseline ${2:+--variant $2}"
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/kt -o kt --output-format csv -- $B > $O/kt.log 2>&1
 timeout -k 10 240 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY -d $O/p1 -o p1 --output-format csv -- $B > $O/p1.log 2>&1
 timeout -k 10 240 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INST_CYCLES_VMEM GRBM_GUI_ACTIVE SQ_WAIT_INST_ANY SQ_ACTIVE_INST_SCA -d $O/p2 -o p2 --output-format csv -- $B > $O/p2.log 2>&1

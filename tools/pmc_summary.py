@@ -45,6 +45,8 @@ def main():
     ap.add_argument("--key", required=True)
     ap.add_argument("--round", default="r01")
     ap.add_argument("--out", default="profiles")
+    ap.add_argument("--sq", default=None, help="directory of SQ counter passes (SQ_INSTS_VALU / SALU)")
+    ap.add_argument("--envs", type=int, default=65536)
     a = ap.parse_args()
     stats = [r for r in rows(a.kt, "*kernel_stats.csv") if "usv::" in r["Name"]]
     step = [r for r in stats if STEP_RE.search(r["Name"])]
@@ -62,6 +64,14 @@ def main():
         "hbm_bytes_per_launch_raw": round((fetch_kib + write_kib) * 1024),
         "correction": "2 x FETCH_SIZE (16-B/lane reads, gfx950) + WRITE_SIZE",
     }
+    if a.sq:          # wave-instruction counts per launch, for roofline.valu_frac (bench.py)
+        for name in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVES"):
+            try:
+                v, _ = counter(a.sq, name)
+            except SystemExit:
+                continue
+            summ[name.lower() + "_per_launch"] = v
+            summ[name.lower() + "_per_env"] = v / a.envs
     os.makedirs(a.out, exist_ok=True)
     json.dump(summ, open(os.path.join(a.out, f"{a.round}_summary.json"), "w"), indent=1)
     agg_p = os.path.join(a.out, "pmc_summary.json")
@@ -69,6 +79,9 @@ def main():
     agg[a.key] = {"hbm_bytes_per_launch": summ["hbm_bytes_per_launch"],
                   "hbm_bytes_per_launch_raw": summ["hbm_bytes_per_launch_raw"],
                   "step_kernel_avg_ns": summ["step_kernel_avg_ns"], "round": a.round}
+    for k in ("sq_insts_valu_per_launch", "sq_insts_salu_per_launch"):
+        if k in summ:
+            agg[a.key][k] = summ[k]
     json.dump(agg, open(agg_p, "w"), indent=1)
     print(json.dumps(summ, indent=1))
 

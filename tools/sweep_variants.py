@@ -1,4 +1,4 @@
-"""Step-kernel variant sweep (envs per block x lidar variant) on one GPU.
+"""Step-kernel variant sweep (usv_set_kernel_variant: envs per block, lidar variant, kind) on one GPU.
 
 For every variant: check the outputs of a short seeded rollout are bit-identical to the first
 variant's, then time back-to-back launches with HIP events.  Prints one JSON line per variant.
@@ -19,8 +19,8 @@ import gym_usv_amd  # noqa: E402
 
 
 def run(variant, args, acts):
-    os.environ["USV_STEP_VARIANT"] = variant
-    env = gym_usv_amd.make_vec(args.env_id, args.envs, seed=3, precision=args.precision)
+    env = gym_usv_amd.make_vec(args.env_id, args.envs, seed=3, precision=args.precision, kernel_variant=variant,
+                               copy=False)
     env.reset(seed=3)
     outs = []
     for k in range(16):
@@ -52,7 +52,8 @@ def main():
     ap.add_argument("--steps", type=int, default=500)
     ap.add_argument("--env-id", default="usv-simple")
     ap.add_argument("--precision", default="f32")
-    ap.add_argument("--variants", default="64,0 32,1 32,3 16,5 32,5 64,5 16,7 32,7 64,7")
+    ap.add_argument("--variants", default="64,7,1 16,7,1 16,7,2 128,7,4 128,7,5 16,7,5",
+                    help="epb,lid,kind triples (include/usv_hip.h usv_set_kernel_variant)")
     args = ap.parse_args()
     g = torch.Generator(device="cuda").manual_seed(0)
     acts = [torch.rand(args.envs, 2, device="cuda", generator=g) * torch.tensor([0.8, 2.0], device="cuda")

@@ -1,6 +1,6 @@
 """Per-wave timeline of the fused wave kernel (kind 1) from the diagnostic build's stamps.
 
-    hipcc ... -DUSV_DIAG_STAMPS -o diag/stamps.so gym-usv_amd/csrc/usv_kernels.hip
+    bash tools/build_diag.sh STAMPS   (-> diag/stamps.so)
     USV_LIB_PATH=diag/stamps.so python tools/wave_timeline.py [--envs 65536] [--variant 16,7,1]
 
 Stamps (s_memrealtime, 100 MHz, per wave): 0 start, 1 dynamics done, 2 after the block barrier,
@@ -30,11 +30,10 @@ def main():
     ap.add_argument("--warm", type=int, default=100)
     ap.add_argument("--env-id", default="usv-simple")
     args = ap.parse_args()
-    os.environ["USV_STEP_VARIANT"] = args.variant
     import gym_usv_amd
     lib = gym_usv_amd.load_library()
     lib.usv_diag_stamps.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
-    env = gym_usv_amd.make_vec(args.env_id, args.envs, seed=1)
+    env = gym_usv_amd.make_vec(args.env_id, args.envs, seed=1, kernel_variant=args.variant, copy=False)
     env.reset(seed=1)
     g = torch.Generator(device="cuda").manual_seed(0)
     lo, span = torch.tensor([0.2, -1.0], device="cuda"), torch.tensor([0.8, 2.0], device="cuda")
