@@ -101,14 +101,14 @@ __device__ __forceinline__ void fx_sincos(float x, float* s, float* c) {
 }
 __device__ __forceinline__ void fx_sincos(double x, double* s, double* c) { sincos(x, s, c); }
 __device__ __forceinline__ float  fx_exp(float x)  { return __expf(x); }
-// atan2 for the f32 step's angle to target: octant reduction with an IEEE quotient and a degree-15
+// atan2 for the f32 step's angle to target: octant reduction with a reciprocal quotient and a degree-15
 // odd minimax polynomial (|err| <= 1.4e-7 rad on [0, 1] evaluated in float, ~1 ulp of pi after the
 // octant fold): ~20 VALU instead of libm's branchy atan2f on the phase-1 critical path.  The f64
 // build keeps libm.
 __device__ __forceinline__ float fx_atan2(float y, float x) {
   const float ax = fabsf(x), ay = fabsf(y);
   const float mx = fmaxf(ax, ay), mn = fminf(ax, ay);
-  const float t = mx > 0.0f ? mn / mx : 0.0f;
+  const float t = mx > 0.0f ? mn * __builtin_amdgcn_rcpf(mx) : 0.0f;   // hardware reciprocal, 1 ulp
   const float s = t * t;
   float p = -0.004054558929055929f;
   p = fmaf(p, s, 0.021862929686903954f);

@@ -4,7 +4,8 @@
     USV_LIB_PATH=diag/stamps.so python tools/wave_timeline.py [--envs 65536] [--variant 16,7,1]
 
 Stamps (s_memrealtime, 100 MHz, per wave): 0 start, 1 dynamics done, 2 after the block barrier,
-3 scan done, 6 end; slot 7 = HW_ID | XCC_ID << 32.  Diagnostic only.
+3 scan done, 5 first pair done (block queue), 6 end; slot 4 = pairs scanned (block queue); slot 7 =
+HW_ID | XCC_ID << 32.  Diagnostic only.
 """
 import argparse
 import ctypes
@@ -134,6 +135,23 @@ def main():
                                round(float(ce[i]), 2)] for i in slow]
         pairs_w = raw[:, 4].astype(np.int64)
         out["pairs_per_wave"] = pct(pairs_w)
+        # per role (older / younger block of a CU): phase-1 end (stamp 1), barrier exit (2), end (6),
+        # pairs scanned per wave
+        role = np.zeros(nw, np.int64)
+        for c in cus:
+            bl = sorted(per_cu[c])
+            if len(bl) == 2:
+                role[blk_id == bl[1][2]] = 1
+        for nm, r in (("older", 0), ("younger", 1)):
+            m = role == r
+            fp = (raw[m, 5].astype(np.int64) - int(t0)) / 100.0       # stamp 5: first pair done
+            out[nm + "_roles"] = {"start": pct(st[m, 0]), "dyn_end": pct(st[m, 1]), "barrier_exit": pct(st[m, 2]),
+                                  "first_pair_end": pct(fp),
+                                  "end": pct(st[m, 4]), "pairs": pct(pairs_w[m]),
+                                  "pairs_total_per_block": float(pairs_w[m].sum() / max(1, m.sum() // wpb))}
+        # pairs finished by both blocks of a CU over time is not stamped; the wave ends are
+        ends = np.sort(st[:, 4])
+        out["wave_end_deciles_us"] = np.percentile(ends, np.arange(0, 101, 10)).round(2).tolist()
     print(json.dumps(out))
 
 
