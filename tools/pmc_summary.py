@@ -28,8 +28,18 @@ def rows(d, pattern):
     return list(csv.DictReader(open(f[0])))
 
 
+def all_rows(d, pattern):
+    out = []
+    for f in sorted(glob.glob(os.path.join(d, "**", pattern), recursive=True)):
+        out += list(csv.DictReader(open(f)))
+    if not out:
+        raise SystemExit(f"no {pattern} under {d}")
+    return out
+
+
 def counter(d, name, skip=5):
-    vals = [float(r["Counter_Value"]) for r in rows(d, "*counter_collection.csv")
+    """Mean per dispatch of `name` over every counter CSV under `d` (one per --pmc pass)."""
+    vals = [float(r["Counter_Value"]) for r in all_rows(d, "*counter_collection.csv")
             if STEP_RE.search(r["Kernel_Name"]) and r["Counter_Name"] == name]
     if not vals:
         raise SystemExit(f"no step-kernel {name} samples under {d}")
