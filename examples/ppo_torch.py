@@ -207,7 +207,7 @@ class PPO:
                 stats.append(torch.stack((pg.detach(), vl.detach(), ent.detach())))
         s = torch.stack(stats).mean(0).tolist()
         return {"policy_loss": s[0], "value_loss": s[1], "entropy": s[2],
-                "std_mean": float(self.model.log_std.exp().mean())}
+                "std_mean": float(self.model.log_std.detach().exp().mean())}
 
     def episode_stats(self):
         out = {"mean_abs_ye": float(torch.stack(self.abs_ye).mean())} if self.abs_ye else {}
