@@ -116,7 +116,9 @@ struct QProf { __device__ void mark(int) {} __device__ void count(int, unsigned 
 __device__ __forceinline__ void qprof_flush(QProf*) {}
 #endif
 // Output rows (obs, reward) are stored write-through (sc1: the line leaves the XCD's L2 as it is
-// written, instead of being written back at the kernel boundary).  The next launch on the stream
+// written, instead of being written back at the kernel boundary) where a wave stores contiguous
+// bytes (a row's sensors, consecutive envs' rewards); lane-per-env stores to 64 different rows stay
+// plain, so that L2 merges them.  The next launch on the stream
 // then starts without a write-back of ~40 MB of dirty obs lines: 20.9 -> 19.4 us per step at
 // 65 536 envs (back-to-back launches, tools/exp_ab.sh); the same policy for the dynamics' state
 // stores measured slower (19.8 us), non-temporal stores in between (20.1 us).
@@ -1097,6 +1099,93 @@ __device__ __forceinline__ void lidar_window_d(double dx, double dy, double key,
   out.rd1 = reading_of(t1.x, t1.y, bj1, a, b, r2);
 }
 
+// Two envs per wave for the f64 window lidar (<= 32 obstacles each), lidar_window_d's arithmetic with
+// lidar_window2's layout: lanes 0..31 hold env A's obstacles, lanes 32..63 env B's, each lane in the
+// ray-0 frame of its own env's pose; both envs' (obstacle, ray) pairs go into one expanded list whose
+// slots are env A's rays then env B's [256].  The winner payload's low 6 bits are the obstacle lane
+// (0..63, so it names the env too), and each reading is recomputed from the winner's (a, b, r^2) as
+// lidar_brute does: readings bit-identical to lidar_window_d and to the brute loop.
+__device__ __forceinline__ void lidar_wave2_d(const double* rows, int os, int nl, double px, double py, double sp,
+                                              double cp, const double2* rayoff, unsigned long long* slot,
+                                              int* mark, double4* rec, Scan<double>& A, Scan<double>& B) {
+  const int l = lane_id();
+  const int jl = l & 31;
+  const bool valid = jl < nl;
+  const double* rb = rows + (l >= 32 ? 3 * os : 0);
+  // read unconditionally (lanes past their env's obstacles get padding; every use is masked by valid)
+  const double ox = rb[jl], oy = rb[os + jl], rr = rb[2 * os + jl];
+  const double dx = ox - px, dy = oy - py;
+  const double d = l_sqrt(m_fma(dx, dx, dy * dy));
+  const double key = valid ? d - rr : big<double>();                          // simple_env.py:205-206
+  const unsigned long long vm = ballot(valid);
+  const unsigned long long tb = vm & ballot(key < kTermDist);                  // :334
+  A.term = (unsigned)tb != 0u; B.term = (unsigned)(tb >> 32) != 0u;
+  A.far = B.far = false;
+  const bool far = (vm & ballot(d >= 0.99 * kSensorMax)) != 0;               // :458 matters
+  double a, b;
+  to_ray0(dx, dy, ray_c(cp, sp, double(kStartC), double(kStartS)), ray_s(cp, sp, double(kStartC), double(kStartS)), a, b);
+  const double r2 = rr * rr;
+  const float inv = (float)(1.0 / kRes);
+  float pr = fast_atan2((float)b, (float)a) * inv;    // branch cut in the blind sector (lidar_window2)
+  pr = pr < -32.5f ? pr + 192.0f : pr;
+  const float margin = (float)(kWinMargin * kRes);
+  const float x = fminf((float)rr * __builtin_amdgcn_rcpf((float)d), 1.0f);
+  const float hr = (fmaf((float)(kPi / 2 - 1) * x, x * x, x) + margin) * inv;
+  const bool wide = (d <= rr * 1.001) | (hr >= 32.5f);
+  const int lo = wide ? 0 : max(0, (int)ceilf(pr - hr));
+  const int hi = wide ? 127 : min(127, (int)floorf(pr + hr));
+  const int cnt = valid ? max(0, hi - lo + 1) : 0;
+  const int incl = wave_incl_scan(cnt);
+  const int off = wave_excl_of(incl);
+  const int W = __builtin_amdgcn_readlane(incl, 63);
+  // mark: owner lane + 1 in the high bits, slot offset (env B: + 128) in the low bits
+  const int mk0 = ((l + 1) << 16) | (lo - off + (l >= 32 ? 128 : 0) + 32768);
+  const unsigned long long kq = (ord_key64(key) & ~63ull) | (unsigned long long)l;
+  // per-obstacle record (a, b, r^2, key | lane) in LDS: a pair reads its owner's with two ds_read_b128
+  rec[l] = make_double4(a, b, r2, __longlong_as_double((long long)kq));
+  const int mpass = cnt > 0 ? off >> 6 : -1;
+  int carry = 0;
+  for (int base = 0, pass = 0; base < W; base += kWave, ++pass) {   // wave-uniform pass count
+    if (mpass == pass) mark[off & (kWave - 1)] = mk0;   // marks of earlier passes are <= carry
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const int mk = max(wave_incl_max_asm(mark[l]), carry);
+    carry = __builtin_amdgcn_readlane(mk, 63);
+    const int q = base + l;
+    const int jj = max((mk >> 16) - 1, 0);
+    const int si = (q + (mk & 0xffff) - 32768) & 255;
+    const double4 o = rec[jj];                         // owner's (a, b, r^2, key | lane)
+    const unsigned long long jk = (unsigned long long)__double_as_longlong(o.w);
+    const double2 cs = rayoff[si & 127];
+    const double proj = m_fma(o.x, cs.x, o.y * cs.y);  // ray_pair's arithmetic
+    const double perp = m_fma(o.x, cs.y, -(o.y * cs.x));
+    const double delta = m_fma(-perp, perp, o.z);
+    bool hit = (q < W) & (proj >= 0.0) & (delta >= 0.0);
+    if (far) hit = hit && (proj - l_sqrt(delta)) < double(kSensorMax);       // :458 (wave-uniform)
+    if (hit) atomicMin(&slot[si], jk);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  const unsigned long long v0 = slot[l], v1 = slot[l + 64], v2 = slot[128 + l], v3 = slot[192 + l];
+  slot[l] = kSlotArm; slot[l + 64] = kSlotArm; slot[128 + l] = kSlotArm; slot[192 + l] = kSlotArm;
+  mark[l] = 0;
+  // reading of the winner (reading_of's arithmetic, the winner's record from LDS)
+  auto reading = [&](double c, double sn, unsigned long long v) {
+    const double4 w = rec[(int)(v & 63)];
+    const double proj = m_fma(w.x, c, w.y * sn);
+    const double perp = m_fma(w.x, sn, -(w.y * c));
+    const double delta = m_fma(-perp, perp, w.z);
+    return v != kSlotArm ? proj - l_sqrt(delta) : double(kSensorMax);     // :457-459
+  };
+  const double2 t0 = rayoff[l], t1 = rayoff[l + 64];
+  A.rd0 = reading(t0.x, t0.y, v0);
+  A.rd1 = reading(t1.x, t1.y, v1);
+  B.rd0 = reading(t0.x, t0.y, v2);
+  B.rd1 = reading(t1.x, t1.y, v3);
+  // the records are read by every lane above before the caller's next writes to this buffer (the
+  // wave's LDS instructions complete in order)
+}
+
 template <typename R, int LID, typename Row>
 __device__ __forceinline__ void lidar_wave(const Row& E, int n, R px, R py, R sp, R cp,
                                            const typename Vec2<R>::T* rayoff, unsigned long long* slot,
@@ -1159,9 +1248,9 @@ __host__ __device__ constexpr size_t align16(size_t b) { return (b + 15) & ~(siz
 __host__ __device__ constexpr int obst_stride(int cap) { return (cap + 3) & ~3; }
 template <typename R> __host__ __device__ constexpr int row_bytes(int cap) { return 3 * obst_stride(cap) * (int)sizeof(R); }
 template <typename R> __host__ __device__ constexpr size_t wave_tab_bytes() { return kSensors * 2 * sizeof(R); }
-// two rows, and at least the 64 x 16-B per-obstacle records lidar_window2 leaves in the buffer
+// two rows, and at least the 64 per-obstacle records (a, b, r^2, key) lidar_window2 / lidar_wave2_d leave in it
 template <typename R> __host__ __device__ constexpr size_t scan_rowbuf_bytes(int cap) {
-  return align16(std::max((size_t)2 * row_bytes<R>(cap), (size_t)1024));
+  return align16(std::max((size_t)2 * row_bytes<R>(cap), (size_t)64 * 4 * sizeof(R)));
 }
 template <typename R> __host__ __device__ constexpr size_t lds_scan_slice(int cap) {
   return 256 * 8 + 64 * 4 + 2 * scan_rowbuf_bytes<R>(cap);
@@ -1222,7 +1311,7 @@ __device__ __forceinline__ ScanLds<R> scan_lds(char* lds, int wave, int cap) {
 }
 // envs per scan iteration: two on the f32 window path (<= 32 obstacle lanes per env)
 template <typename R, int LID> __device__ __forceinline__ int scan_step(int cap) {
-  return (std::is_same<R, float>::value && (LID & kLidWindow) != 0 && cap <= 32) ? 2 : 1;
+  return ((LID & kLidWindow) != 0 && cap <= 32) ? 2 : 1;     // lidar_wave2 / lidar_wave2_d
 }
 // Issue the prologue DMAs (ray table by wave 0, the first iteration's rows) and arm the slots.
 template <typename R, int LID>
@@ -1326,6 +1415,26 @@ __device__ __forceinline__ void scan_envs(const State<R>& S, const IO<R>& io, co
         continue;
       }
     }
+    if constexpr (std::is_same<R, double>::value && (LID & kLidWindow) != 0) {
+      if (step == 2) {                             // as above, f64 arithmetic (lidar_wave2_d)
+        const bool hasB = k + 1 < ne;
+        const bool hb = lane_id() >= 32;
+        const int kl = hb ? k + 1 : k;
+        const int kc = hasB ? kl : k;
+        const double lpx = __shfl(P.x, kc, kWave), lpy = __shfl(P.y, kc, kWave);
+        const double lsp = __shfl(P.z, kc, kWave), lcp = __shfl(P.w, kc, kWave);
+        const int lnl = (hb && !hasB) ? 0 : __shfl(nl, kc, kWave);
+        Scan<double> sa, sb;
+        // the records overwrite this iteration's rows once every lane has read them (in-order LDS)
+        lidar_wave2_d(cur, obst_stride(cap), lnl, lpx, lpy, lsp, lcp, L.rayoff, L.slot, L.mark,
+                      reinterpret_cast<double4*>(cur), sa, sb);
+        prof.mark(2);
+        emit(k, sa);
+        if (hasB) emit(k + 1, sb);
+        prof.mark(3);
+        continue;
+      }
+    }
     Scan<R> sc;
     const int os = obst_stride(cap);
     lidar_wave<R, LID>(RowSoA<R>{cur, cur + os, cur + 2 * os}, __builtin_amdgcn_readlane(nl, k), bcast(P.x, k),
@@ -1386,7 +1495,7 @@ __device__ __forceinline__ void step_body_wave(const State<R>& S, const IO<R>& i
                              io.info ? io.info + (size_t)e * USV_INFO_DIM : nullptr);
     float* row = io.obs + (size_t)e * kObsDim;
 #pragma unroll
-    for (int i = 0; i < kHdr; ++i) st_out(row + i, hdr[i]);
+    for (int i = 0; i < kHdr; ++i) row[i] = hdr[i];   // lane-per-env rows: plain stores (L2 merges them)
     nl = S.I(I_NOBS)[e];
   }
   const unsigned trunc_m = (unsigned)ballot(trunc);
@@ -1430,7 +1539,7 @@ __global__ __launch_bounds__(kBlock) void dyn_kernel(State<R> S, IO<R> io) {
                              io.info ? io.info + (size_t)e * USV_INFO_DIM : nullptr);
   float* row = io.obs + (size_t)e * kObsDim;
 #pragma unroll
-  for (int i = 0; i < kHdr; ++i) row[i] = hdr[i];
+  for (int i = 0; i < kHdr; ++i) row[i] = hdr[i];     // lane-per-env rows: plain stores (L2 merges them)
   S.pose[2 * (size_t)e] = R4<R>{px, py, sp, cp};
   S.pose[2 * (size_t)e + 1] = R4<R>{partial, R(S.I(I_NOBS)[e]), R(trunc ? 1 : 0), R(0)};
   io.rew[e] = partial;
@@ -1479,6 +1588,14 @@ template <typename R, int MODE, int EPW, int LID, int WPB>
 __global__ __launch_bounds__(kWave * WPB) void scan_kernel(State<R> S, IO<R> io) {
   scan_body<R, MODE, EPW, LID, WPB>(S, io);
 }
+
+// f64 scan compiled for more waves per SIMD (the uncapped f64 scan takes 141 VGPRs: 3 waves)
+#ifndef USV_F64_SCAN_WAVES
+#define USV_F64_SCAN_WAVES 4
+#endif
+template <typename R, int MODE, int EPW, int LID, int WPB>
+__global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(USV_F64_SCAN_WAVES, USV_F64_SCAN_WAVES)))
+void scan_kernel_d(State<R> S, IO<R> io) { scan_body<R, MODE, EPW, LID, WPB>(S, io); }
 
 // ---- block-queue step (f32 window lidar, cap <= 32): 1024-thread blocks of 16 waves own
 // kQE = 128 envs each; the block's env pairs are pulled from an LDS counter.  VALU issue on a
@@ -2356,6 +2473,9 @@ void* pick_scan_lid(int lid) {
     if (lid == 3) return (void*)&scan_kernel_tight<R, MODE, EPW, 3, WPB>;
     return (void*)&scan_kernel_tight<R, MODE, EPW, 7, WPB>;
   }
+  if constexpr (std::is_same<R, double>::value && MODE == USV_MODE_SIMPLE) {
+    if (lid == 7) return (void*)&scan_kernel_d<R, MODE, EPW, 7, WPB>;
+  }
   if (lid == 0) return (void*)&scan_kernel<R, MODE, EPW, 0, WPB>;
   if (lid == 3) return (void*)&scan_kernel<R, MODE, EPW, 3, WPB>;
   return (void*)&scan_kernel<R, MODE, EPW, 7, WPB>;
@@ -2723,6 +2843,8 @@ int usv_create(const usv_config* cfg, int32_t device, void** out) {
   } else if (queue) {
     h->kind = 5;                        // block-queue step: 16-wave blocks of 128 envs, or 8-wave blocks
     h->epb = cfg->num_envs < kQSmallBelow ? kQE_S : kQE;   // of 16 below kQSmallBelow envs
+  } else if (cfg->precision == USV_F64 && cfg->lidar_algo == USV_LIDAR_WINDOW && cfg->obstacle_cap <= 32) {
+    h->kind = 2; h->epb = 32;           // f64: full-width dynamics, then the two-env wave scan (8 envs/wave)
   } else { h->kind = 1; h->epb = 64; }
   h->prio = (h->kind == 4 || h->kind == 5) ? 0 : 1;   // the ramp helps static splits only
   if (const int rc = queue_lds_attr(h); rc != USV_OK) { delete h; return rc; }
