@@ -1,11 +1,11 @@
-# Per-CU timeline of the block-queue step (diag/stamps.so): which CUs end the launch, and whether
+# Per-CU timeline of the block-queue step (diagbuild/stamps.so): which CUs end the launch, and whether
 # their end follows their dispatch time.  Build first: bash tools/build_diag.sh STAMPS.
 set -e
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
 mkdir -p gpurun_out/cutl
 for r in 1 2; do
-  USV_LIB_PATH=${LIB:-diag/stamps.so} timeout -k 10 120 python tools/wave_timeline.py --variant 128,7,5 > gpurun_out/cutl/run$r.json 2> gpurun_out/cutl/run$r.err
+  USV_LIB_PATH=${LIB:-diagbuild/stamps.so} timeout -k 10 120 python tools/wave_timeline.py --variant 128,7,5 > gpurun_out/cutl/run$r.json 2> gpurun_out/cutl/run$r.err
 done
 python -c "
 import json

@@ -1,7 +1,7 @@
 """Per-wave section cycles of the block-queue step from the diagnostic build (-DUSV_DIAG_QPROF).
 
-    bash tools/build_diag.sh QPROF   (-> diag/qprof.so)
-    USV_LIB_PATH=diag/qprof.so python tools/qprof.py [--envs 65536]
+    bash tools/build_diag.sh QPROF   (-> diagbuild/qprof.so)
+    USV_LIB_PATH=diagbuild/qprof.so python tools/qprof.py [--envs 65536]
 
 Slots (shader-clock cycles per wave, summed over the wave's pairs): 10 phase 1 (start -> barrier),
 0 barrier wait, 1 iteration top (ticket, DMA issue, record reads), 2 lidar setup + scan, 3 passes,

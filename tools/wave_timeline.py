@@ -1,7 +1,7 @@
 """Per-wave timeline of the fused wave kernel (kind 1) from the diagnostic build's stamps.
 
-    bash tools/build_diag.sh STAMPS   (-> diag/stamps.so)
-    USV_LIB_PATH=diag/stamps.so python tools/wave_timeline.py [--envs 65536] [--variant 16,7,1]
+    bash tools/build_diag.sh STAMPS   (-> diagbuild/stamps.so)
+    USV_LIB_PATH=diagbuild/stamps.so python tools/wave_timeline.py [--envs 65536] [--variant 16,7,1]
 
 Stamps (s_memrealtime, 100 MHz, per wave): 0 start, 1 dynamics done, 2 after the block barrier,
 3 scan done, 5 first pair done (block queue), 6 end; slot 4 = pairs scanned (block queue); slot 7 =
