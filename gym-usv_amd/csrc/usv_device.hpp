@@ -281,6 +281,22 @@ __device__ __forceinline__ void perturb_force(int pstep, double& fx, double& fy)
   fy = cos(t + k + 10.0) * 5.0;
 }
 
+// Trapezoid update H (a + b) / 2 + c (usv_asmc.py:87-88, 129, 143-146, 228-234).  f32 build: one
+// fused multiply-add by H / 2 (the product H (a + b) / 2 equals (a + b) * fl(H / 2) before the final
+// rounding); f64 build: the reference's operation order, bit-exact vs the oracle.
+__device__ __forceinline__ float  asmc_trap(float a, float b, float c)  { return fmaf(a + b, 0.005f, c); }
+__device__ __forceinline__ double asmc_trap(double a, double b, double c) { return H * (a + b) / 2.0 + c; }
+// k * np.sign(d) for the adaptive gains (usv_asmc.py:137-140); f32: copysign (np.sign(0) = 0 kept)
+__device__ __forceinline__ float  asmc_ksign(float k, float d)  { return d != 0.0f ? copysignf(k, d) : 0.0f; }
+__device__ __forceinline__ double asmc_ksign(double k, double d) { return k * m_sign(d); }
+// -K sqrt|sig| sign(sig) (usv_asmc.py:150-151); f32: copysign of the root (equal but for the sign of
+// a zero result, which the following subtraction absorbs)
+__device__ __forceinline__ float  asmc_root(float K, float sig)  { return -K * copysignf(__builtin_amdgcn_sqrtf(fabsf(sig)), sig); }
+__device__ __forceinline__ double asmc_root(double K, double sig) { return -K * sqrt(fabs(sig)) * m_sign(sig); }
+// wrap_once (usv_asmc.py:120); f32: e - copysign(2 pi, e), bit-identical to sign(e) (|e| - 2 pi)
+__device__ __forceinline__ float  asmc_wrap(float e)  { return fabsf(e) > float(kPi) ? e - copysignf(float(2 * kPi), e) : e; }
+__device__ __forceinline__ double asmc_wrap(double e) { return wrap_once(e); }
+
 template <typename R>
 __device__ __forceinline__ void asmc_substep(R (&s)[kAsmcN], R a0, R a1, R& x, R& y, R& psi,
                                              R& u, R& v, R& r, int pstep = 0, bool perturb = false) {
@@ -293,8 +309,8 @@ __device__ __forceinline__ void asmc_substep(R (&s)[kAsmcN], R a0, R a1, R& x, R
   R r_d = fx_cdiv(psi_d - s[0], H);                                        // :84
   s[0] = psi_d;
   const R o_dd = ((r_d - s[1]) * R(F1) - R(F3) * s[2]) * R(F2);            // :86
-  const R o_d = R(H) * (o_dd + s[3]) / R(2) + s[2];                        // :87
-  const R o = R(H) * (o_d + s[2]) / R(2) + s[1];                           // :88
+  const R o_d = asmc_trap(o_dd, s[3], s[2]);                        // :87
+  const R o = asmc_trap(o_d, s[2], s[1]);                           // :88
   s[1] = o; s[2] = o_d; s[3] = o_dd;
   r_d = o;                                                                 // :89
   const bool fast = m_abs(u) > R(1.2);                                     // :95-99
@@ -304,20 +320,20 @@ __device__ __forceinline__ void asmc_substep(R (&s)[kAsmcN], R a0, R a1, R& x, R
   const R yr = R(YR_K) * vmag, nv = R(NV_K) * vmag, nr = R(NR_K) * vmag;  // :103-108
   const R f_u = fx_cdiv(R(MASS - Y_V_DOT) * v * r + (xuu * m_abs(u) + xu * u), MASS - X_U_DOT);  // :113
   const R f_psi = fx_cdiv(R(-X_U_DOT + Y_V_DOT) * u * v + nr * r, IZ - N_R_DOT);                 // :115
-  const R e_psi = wrap_once(psi_d - psi);                                  // :119-120
+  const R e_psi = asmc_wrap(psi_d - psi);                                  // :119-120
   const R e_psi_dot = r_d - r;                                             // :121
   const R e_u = a0 - u;                                                    // :128
-  s[13] = R(H) * (e_u + s[10]) / R(2) + s[13];                             // :129 e_u_int
+  s[13] = asmc_trap(e_u, s[10], s[13]);                             // :129 e_u_int
   s[10] = e_u;
   const R sig_u = e_u + R(LAMBDA_U) * s[13];                               // :133
   const R sig_p = e_psi_dot + R(LAMBDA_PSI) * e_psi;                       // :134
-  const R kdu = s[14] > R(KMIN_U) ? R(K_U) * m_sign(m_abs(sig_u) - R(MU_U)) : R(KMIN_U);       // :137
-  const R kdp = s[15] > R(KMIN_PSI) ? R(K_PSI) * m_sign(m_abs(sig_p) - R(MU_PSI)) : R(KMIN_PSI);
-  s[14] = R(H) * (kdu + s[11]) / R(2) + s[14];                             // :143
-  s[15] = R(H) * (kdp + s[12]) / R(2) + s[15];                             // :146
+  const R kdu = s[14] > R(KMIN_U) ? asmc_ksign(R(K_U), m_abs(sig_u) - R(MU_U)) : R(KMIN_U);       // :137
+  const R kdp = s[15] > R(KMIN_PSI) ? asmc_ksign(R(K_PSI), m_abs(sig_p) - R(MU_PSI)) : R(KMIN_PSI);
+  s[14] = asmc_trap(kdu, s[11], s[14]);                             // :143
+  s[15] = asmc_trap(kdp, s[12], s[15]);                             // :146
   s[11] = kdu; s[12] = kdp;
-  const R ua_u = -s[14] * fx_sqrt(m_abs(sig_u)) * m_sign(sig_u) - R(K2_U) * sig_u;   // :150
-  const R ua_p = -s[15] * fx_sqrt(m_abs(sig_p)) * m_sign(sig_p) - R(K2_PSI) * sig_p; // :151
+  const R ua_u = asmc_root(s[14], sig_u) - R(K2_U) * sig_u;   // :150
+  const R ua_p = asmc_root(s[15], sig_p) - R(K2_PSI) * sig_p; // :151
   const R tx = (R(LAMBDA_U) * e_u - f_u - ua_u) * R(MASS - X_U_DOT);      // :154
   const R tz = (R(LAMBDA_PSI) * e_psi - f_psi - ua_p) * R(IZ - N_R_DOT);  // :155
   const R tport = tx / R(2) + fx_cdiv(tz, B_TH);                           // :158
@@ -351,15 +367,101 @@ __device__ __forceinline__ void asmc_substep(R (&s)[kAsmcN], R a0, R a1, R& x, R
   const R ud = R(MI00) * rhs0;                                             // :226
   const R vd = R(MI11) * rhs1 + R(MI12) * rhs2;
   const R rd = R(MI21) * rhs1 + R(MI22) * rhs2;
-  u = R(H) * (ud + s[7]) / R(2) + u;                                       // :228-229
-  v = R(H) * (vd + s[8]) / R(2) + v;
-  r = R(H) * (rd + s[9]) / R(2) + r;
+  u = asmc_trap(ud, s[7], u);                                       // :228-229
+  v = asmc_trap(vd, s[8], v);
+  r = asmc_trap(rd, s[9], r);
   s[7] = ud; s[8] = vd; s[9] = rd;
   const R xd = cp * u - sp * v, yd = sp * u + cp * v, pd = r;              // :233
-  x = R(H) * (xd + s[4]) / R(2) + x;                                       // :234
-  y = R(H) * (yd + s[5]) / R(2) + y;
-  psi = R(H) * (pd + s[6]) / R(2) + psi;
+  x = asmc_trap(xd, s[4], x);                                       // :234
+  y = asmc_trap(yd, s[5], y);
+  psi = asmc_trap(pd, s[6], psi);
   s[4] = xd; s[5] = yd; s[6] = pd;
+}
+
+
+// f32 build of asmc_substep: the same law with its algebra folded.  Each rewrite is an identity in
+// real arithmetic, so the float result differs from the reference-order evaluation by rounding
+// only (the f64 build keeps asmc_substep above, bit-exact vs the oracle):
+//  * the thruster split and its recombination (usv_asmc.py:158-159, 176) is the identity
+//    T = (Tx, 0, Tz);
+//  * Tx = (m - Xu')(lambda_u e_u - f_u - ua_u) with f_u = [...] / (m - Xu') (:113, :154): the
+//    division and the multiplication cancel (likewise Iz - Nr' in Tz, :115, :155);
+//  * C(nu) (:201-211): c20 = -c02 and c21 = -c12; D(nu) (:213-223): each entry one linear form in
+//    |v|, |r| and |nu| with the scale factors of :101-108 folded into its coefficients;
+//  * trapezoids H (a + b) / 2 + c as one fma by H / 2; ((r_d - o) F1 - F3 o') F2 with F = 2 as
+//    4 ((r_d - o) - o') (:86; bit-identical); np.sign products as copysign.
+__device__ __forceinline__ void asmc_substep_f32(float (&s)[kAsmcN], float a0, float a1, float& x, float& y,
+                                                 float& psi, float& u, float& v, float& r, int pstep = 0,
+                                                 bool perturb = false) {
+  constexpr float h2 = float(H / 2);
+  const float au = fabsf(u), av = fabsf(v), ar = fabsf(r);
+  const float vmag = __builtin_amdgcn_sqrtf(fmaf(u, u, v * v));
+  // yaw channel: LOS heading, third-order filter, sliding surface (:72-89, :119-121, :134)
+  const float beta = asinf(v * __builtin_amdgcn_rcpf(0.001f + vmag));
+  const float psi_d = psi + beta + a1;
+  const float r_d = (psi_d - s[0]) * float(1.0 / H);
+  s[0] = psi_d;
+  const float o_dd = 4.0f * ((r_d - s[1]) - s[2]);
+  const float o_d = fmaf(o_dd + s[3], h2, s[2]);
+  const float o = fmaf(o_d + s[2], h2, s[1]);
+  s[1] = o; s[2] = o_d; s[3] = o_dd;
+  const float e_psi = asmc_wrap(psi_d - psi);
+  const float sig_p = (o - r) + float(LAMBDA_PSI) * e_psi;
+  // surge channel (:128-133)
+  const float e_u = a0 - u;
+  s[13] = fmaf(e_u + s[10], h2, s[13]);
+  s[10] = e_u;
+  const float sig_u = fmaf(float(LAMBDA_U), s[13], e_u);
+  // adaptive gains (:137-146) and control laws (:150-151)
+  const float kdu = s[14] > float(KMIN_U) ? asmc_ksign(float(K_U), fabsf(sig_u) - float(MU_U)) : float(KMIN_U);
+  const float kdp = s[15] > float(KMIN_PSI) ? asmc_ksign(float(K_PSI), fabsf(sig_p) - float(MU_PSI)) : float(KMIN_PSI);
+  s[14] = fmaf(kdu + s[11], h2, s[14]);
+  s[15] = fmaf(kdp + s[12], h2, s[15]);
+  s[11] = kdu; s[12] = kdp;
+  const float ua_u = asmc_root(s[14], sig_u) - float(K2_U) * sig_u;
+  const float ua_p = asmc_root(s[15], sig_p) - float(K2_PSI) * sig_p;
+  // tau = (Tx, 0, Tz) (:113-176)
+  const bool fast = au > 1.2f;                                                  // :95-99
+  const float xu = fast ? 64.55f : -25.0f;
+  const float xuu = fast ? -70.92f : 0.0f;
+  const float xd_u = fmaf(xuu, au, xu * u);                                     // Xuu |u| + Xu u
+  const float tx = fmaf(float(MASS - X_U_DOT), fmaf(float(LAMBDA_U), e_u, -ua_u),
+                        -fmaf(float(MASS - Y_V_DOT) * v, r, xd_u));
+  const float tz = fmaf(float(IZ - N_R_DOT), fmaf(float(LAMBDA_PSI), e_psi, -ua_p),
+                        -fmaf(float(-X_U_DOT + Y_V_DOT) * u, v, float(NR_K) * vmag * r));
+  // rhs = tau - C(nu) nu - D(nu) nu
+  const float c02 = fmaf(float(-MASS + 2 * Y_V_DOT), v, float(Y_R_DOT + N_V_DOT) * r);
+  const float c12 = float(MASS - X_U_DOT * MASS) * u;
+  const float d00 = fmaf(-xuu, au, -xu);
+  const float md11 = fmaf(float(YV_K + YVV), av, float(YVR) * ar);              // -d11
+  const float md12 = fmaf(float(YR_K), vmag, fmaf(float(YRV), av, float(YRR) * ar));
+  const float md21 = fmaf(float(NV_K), vmag, fmaf(float(NVV), av, float(NVR) * ar));
+  const float md22 = fmaf(float(NR_K), vmag, fmaf(float(NRV), av, float(NRR) * ar));
+  float sp, cp;
+  fx_sincos(psi, &sp, &cp);                                                     // J(psi_old) :179
+  float tt0 = tx, tt1 = 0.0f;
+  if (perturb) {                                                                // T += F @ J (:184-198)
+    double fx, fy;
+    perturb_force(pstep, fx, fy);
+    const float pfx = float(fx), pfy = float(fy);
+    tt0 = tx + (pfx * cp + pfy * sp);
+    tt1 = pfx * -sp + pfy * cp;
+  }
+  const float rhs0 = fmaf(-c02, r, fmaf(-d00, u, tt0));
+  const float rhs1 = fmaf(md11, v, fmaf(md12 - c12, r, tt1));
+  const float rhs2 = fmaf(c02, u, fmaf(c12 + md21, v, fmaf(md22, r, tz)));
+  const float ud = float(MI00) * rhs0;                                          // :226
+  const float vd = fmaf(float(MI11), rhs1, float(MI12) * rhs2);
+  const float rd = fmaf(float(MI21), rhs1, float(MI22) * rhs2);
+  u = fmaf(ud + s[7], h2, u);                                                   // :228-229
+  v = fmaf(vd + s[8], h2, v);
+  r = fmaf(rd + s[9], h2, r);
+  s[7] = ud; s[8] = vd; s[9] = rd;
+  const float xd = fmaf(cp, u, -(sp * v)), yd = fmaf(sp, u, cp * v);          // :233
+  x = fmaf(xd + s[4], h2, x);                                                   // :234
+  y = fmaf(yd + s[5], h2, y);
+  psi = fmaf(r + s[6], h2, psi);
+  s[4] = xd; s[5] = yd; s[6] = r;
 }
 
 }  // namespace usv

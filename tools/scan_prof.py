@@ -49,8 +49,8 @@ def main():
     env.step(a)
     e1.record()
     torch.cuda.synchronize()
-    epw = int(args.variant.split(",")[0])
-    nw = min(16384, (args.envs + epw - 1) // epw)
+    epb = int(args.variant.split(",")[0])           # envs per 4-wave block (kinds 1, 2)
+    nw = min(16384, (args.envs + epb - 1) // epb * 4)
     buf = np.zeros(16384 * 8, dtype=np.uint64)
     assert lib.usv_diag_prof(buf.ctypes.data_as(ctypes.c_void_p), buf.nbytes) == 0
     q = buf.reshape(16384, 8)[:nw].astype(np.float64)

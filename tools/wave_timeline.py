@@ -30,17 +30,21 @@ def main():
     ap.add_argument("--variant", default="16,7,1")
     ap.add_argument("--warm", type=int, default=100)
     ap.add_argument("--env-id", default="usv-simple")
+    ap.add_argument("--precision", default="f32")
     args = ap.parse_args()
     import gym_usv_amd
     lib = gym_usv_amd.load_library()
     lib.usv_diag_stamps.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
-    env = gym_usv_amd.make_vec(args.env_id, args.envs, seed=1, kernel_variant=args.variant, copy=False)
+    env = gym_usv_amd.make_vec(args.env_id, args.envs, seed=1, kernel_variant=args.variant, copy=False,
+                               precision=args.precision)
     env.reset(seed=1)
+    dt = torch.float64 if args.precision == "f64" else torch.float32
     g = torch.Generator(device="cuda").manual_seed(0)
-    lo, span = torch.tensor([0.2, -1.0], device="cuda"), torch.tensor([0.8, 2.0], device="cuda")
+    lo = torch.tensor([0.2, -1.0], device="cuda", dtype=dt)
+    span = torch.tensor([0.8, 2.0], device="cuda", dtype=dt)
     for _ in range(args.warm):
-        env.step(torch.rand(args.envs, 2, device="cuda", generator=g) * span + lo)
-    a = torch.rand(args.envs, 2, device="cuda", generator=g) * span + lo
+        env.step(torch.rand(args.envs, 2, device="cuda", generator=g, dtype=dt) * span + lo)
+    a = torch.rand(args.envs, 2, device="cuda", generator=g, dtype=dt) * span + lo
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
