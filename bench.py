@@ -176,7 +176,10 @@ def cpu_baseline(env_id, seconds, procs, affinity=None, quota=None):
             ratio = cal["ratio_oracle_over_reference"]
             out["calibration"] = {"oracle_over_reference_per_core": ratio,
                                   "reference_equivalent_value": round(rate / ratio, 1),
-                                  "source": "profiles/cpu_calibration.json (tools/calibrate_cpu.py)"}
+                                  "source": "profiles/cpu_calibration.json (tools/calibrate_cpu.py)",
+                                  "note": "reference timed without numba (not importable here), so its "
+                                          "@njit lidar (usv_asmc_ca_env.py:439-440) ran as pure Python: "
+                                          "reference_equivalent_value is a lower bound (unpinned)"}
     return out
 
 

@@ -1600,6 +1600,73 @@ template <typename R, int MODE, int EPW, int LID, int WPB>
 __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(USV_F64_SCAN_WAVES, USV_F64_SCAN_WAVES)))
 void scan_kernel_d(State<R> S, IO<R> io) { scan_body<R, MODE, EPW, LID, WPB>(S, io); }
 
+// ---- fused with block-wide dynamics (kind 3, f64 usv-simple): wave 0 of each 4-wave block runs
+// the dynamics of the block's 4 * EPW <= 64 envs lane-per-env (full width at EPW = 16, as the split
+// dyn_kernel does) and hands each env's pose, obstacle count, partial reward and truncation to its
+// scanning wave through LDS; waves 1..3 meanwhile wait at the barrier with their first rows in
+// flight.  Same per-env arithmetic as kinds 1 and 2, one launch instead of two (no pose records
+// through HBM, no second launch ramp).
+template <typename R> __host__ __device__ constexpr size_t lds_blockdyn_bytes(int cap) {
+  return (lds_scan_bytes<R>(cap) + 31) / 32 * 32 + 2 * kWave * sizeof(R4<R>);
+}
+template <typename R, int MODE, int EPW, int LID>
+__device__ __forceinline__ void step_body_blockdyn(const State<R>& S, const IO<R>& io) {
+  static_assert(kWaves * EPW <= kWave, "one dynamics lane per env of the block");
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);   // wave-uniform (SGPR)
+  const int l = lane_id();
+  const int eb = blockIdx.x * kWaves * EPW;                 // the block's envs eb .. eb+nbe-1
+  const int nbe = min(kWaves * EPW, S.N - eb);
+  const int e0 = eb + wave * EPW;                           // this wave's envs e0 .. e0+ne-1
+  const int ne = min(EPW, S.N - e0);
+  const ScanLds<R> L = scan_lds<R>(lds, wave, S.cap);
+  R4<R>* const rec = reinterpret_cast<R4<R>*>(lds + (lds_scan_bytes<R>(S.cap) + 31) / 32 * 32);
+  Prof prof;
+  USV_STAMP_W(0);
+  USV_STAMP_ID();
+  if (S.prio == 1) __builtin_amdgcn_s_setprio(3);
+  scan_prologue<R, LID>(S, L, wave, e0, ne);
+  if (wave == 0) {
+    // lanes >= nbe recompute env nbe-1 and store identical values to identical addresses (no
+    // divergent memory operations: hipcc's vmcnt bookkeeping stays exact around the DMAs)
+    const int e = eb + min(l, nbe - 1);
+    const float2 a = reinterpret_cast<const float2*>(io.act)[e];
+    float hdr[kHdr];
+    R px, py, sp, cp, partial;
+    bool trunc;
+    env_dynamics<R, MODE>(S, e, a.x, a.y, hdr, px, py, sp, cp, partial, trunc,
+                          io.info ? io.info + (size_t)e * USV_INFO_DIM : nullptr);
+    float* row = io.obs + (size_t)e * kObsDim;
+#pragma unroll
+    for (int i = 0; i < kHdr; ++i) row[i] = hdr[i];         // lane-per-env rows: plain stores
+    rec[l] = R4<R>{px, py, sp, cp};
+    rec[kWave + l] = R4<R>{partial, R(S.I(I_NOBS)[e]), R(trunc ? 1 : 0), R(0)};
+    USV_STAMP_W(1);
+    // the prologue DMA landed: the header stores above were issued after it
+    vm_wait<2>();
+  } else {
+    vm_wait<0>();
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // records + ray table published
+  if (ne <= 0) return;
+  USV_STAMP_W(2);
+  prof.mark(0);
+  const int k = wave * EPW + min(l, ne - 1);                // lane-per-env view of this wave's envs
+  const R4<R> P = rec[k], M = rec[kWave + k];
+  const unsigned trunc_m = (unsigned)ballot(M.z != R(0));
+  unsigned term_m, coll_m;
+  scan_envs<R, MODE, LID>(S, io, L, e0, ne, P, (int)M.y, trunc_m, term_m, coll_m, prof);
+  USV_STAMP_W(3);
+  scan_epilogue<R, MODE>(S, io, e0, ne, M.x, true, term_m, coll_m, trunc_m);
+  prof.mark(5);
+  prof.flush(blockIdx.x * kWaves + wave);
+  USV_STAMP_W(6);
+}
+
+template <typename R, int MODE, int EPW, int LID>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(USV_F64_SCAN_WAVES, USV_F64_SCAN_WAVES)))
+void step_kernel_blockdyn(State<R> S, IO<R> io) { step_body_blockdyn<R, MODE, EPW, LID>(S, io); }
+
 // ---- block-queue step (f32 window lidar, cap <= 32): 1024-thread blocks of 16 waves own
 // kQE = 128 envs each; the block's env pairs are pulled from an LDS counter.  VALU issue on a
 // SIMD is arbitrated by priority, then age, so with a static split the oldest waves finish first
@@ -2556,6 +2623,14 @@ int launch_step_kernels(Handle* h, State<R>& S, const float* act, float* obs, vo
       return USV_OK;
     }
   }
+  if constexpr (std::is_same<R, double>::value) {
+    if (h->kind == 3) {                                     // fused, block-wide dynamics (f64 usv-simple)
+      void* fn = epb == 64 ? (void*)&step_kernel_blockdyn<R, USV_MODE_SIMPLE, 16, 7>
+                           : (void*)&step_kernel_blockdyn<R, USV_MODE_SIMPLE, 8, 7>;
+      HIP_TRY(hipLaunchKernel(fn, dim3((S.N + epb - 1) / epb), dim3(kBlock), args, lds_blockdyn_bytes<R>(S.cap), st));
+      return USV_OK;
+    }
+  }
   if (h->kind == 2) {                                       // split: dynamics, then the wave scan
     void* dyn = simple ? (void*)&dyn_kernel<R, USV_MODE_SIMPLE> : (void*)&dyn_kernel<R, USV_MODE_ASMC_SIMPLE>;
     HIP_TRY(hipLaunchKernel(dyn, dim3((S.N + kBlock - 1) / kBlock), dim3(kBlock), args, 0, st));
@@ -2849,9 +2924,10 @@ int usv_create(const usv_config* cfg, int32_t device, void** out) {
     h->kind = 5;                        // block-queue step: 16-wave blocks of 128 envs, or 8-wave blocks
     h->epb = cfg->num_envs < kQSmallBelow ? kQE_S : kQE;   // of 16 below kQSmallBelow envs
   } else if (cfg->precision == USV_F64 && cfg->lidar_algo == USV_LIDAR_WINDOW && cfg->obstacle_cap <= 32) {
-    // f64: full-width dynamics, then the two-env wave scan; 16 envs/wave from 49 152 envs up (one
-    // round of 4 waves per SIMD at 65 536 envs: 46.1 us against 51.5 for 8 envs/wave), else 8
-    h->kind = 2; h->epb = cfg->num_envs >= 49152 ? 64 : 32;
+    // f64: one launch, wave 0 of each block runs the block's dynamics at full width, then the
+    // two-env wave scan (kind 3); 16 envs/wave from 49 152 envs up (one round of 4 waves per SIMD
+    // at 65 536 envs: 40.3 us, against 47.7 for the split dyn_kernel + scan), else 8
+    h->kind = 3; h->epb = cfg->num_envs >= 49152 ? 64 : 32;
   } else { h->kind = 1; h->epb = 64; }
   h->prio = (h->kind == 4 || h->kind == 5) ? 0 : 1;   // the ramp helps static splits only
   if (const int rc = queue_lds_attr(h); rc != USV_OK) { delete h; return rc; }
@@ -2874,9 +2950,11 @@ int usv_set_kernel_variant(void* hp, int32_t kind, int32_t epb, int32_t lid) {
   const bool wave_ok = kind == 1 && (epb == 16 || epb == 32 || epb == 64) && lid_ok;
   const bool split_ok = kind == 2 && (epb == 8 || epb == 16 || epb == 32 ||
                                       (epb == 64 && lid == 7 && cfg->precision == USV_F64 && cfg->mode == USV_MODE_SIMPLE)) && lid_ok;
+  const bool blockdyn_ok = kind == 3 && (epb == 32 || epb == 64) && lid == 7 && cfg->precision == USV_F64 &&
+                           cfg->mode == USV_MODE_SIMPLE;
   const bool queue_ok = (kind == 4 || kind == 5) && (epb == kQE || (kind == 5 && epb == kQE_S)) && lid == 7 &&
                         cfg->precision == USV_F32 && cfg->obstacle_cap <= 32;
-  if (!(wave_ok || split_ok || queue_ok)) return fail(USV_ERR_ARG, "kernel variant not available for this config");
+  if (!(wave_ok || split_ok || blockdyn_ok || queue_ok)) return fail(USV_ERR_ARG, "kernel variant not available for this config");
   DeviceGuard g(h->device);
   HIP_TRY(hipDeviceSynchronize());                 // launches in flight keep the variant they took
   h->kind = kind;

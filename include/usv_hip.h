@@ -243,7 +243,9 @@ int usv_step_ex(void* handle, const float* act_dev, float* obs_dev, void* rew_de
  * tuning: every variant computes bit-identical outputs, tests/test_gpu_*.py compare them bitwise).
  * No reference counterpart; usv_create picks the tuned default.
  *   kind 1: fused wave kernel (epb 16 | 32 | 64 envs per 256-thread block)
- *   kind 2: split dynamics + wave scan (epb 8 | 16 | 32)
+ *   kind 2: split dynamics + wave scan (epb 8 | 16 | 32; f64 usv-simple window also 64)
+ *   kind 3: one launch, wave 0 of each 4-wave block runs the block's dynamics, then the wave scan
+ *           (f64 usv-simple, window lidar; epb 32 | 64)
  *   kind 4 / 5: split / fused block-queue step (epb 128; kind 5 also 16), f32 window lidar, cap <= 32
  *   lid: lidar variant bits (0 brute, 3 brute + blind-sector skip + unroll, 7 angular window)
  * Waits for in-flight launches first.  USV_ERR_ARG if the handle's config cannot run it. */

@@ -343,7 +343,7 @@ def test_step_variants_bit_identical(env_id, precision):
     ref = None
     queue = ("128,7,4", "128,7,5", "16,7,5") if precision == "f32" else ()   # block queue: f32 only
     if precision == "f64" and env_id == "usv-simple":
-        queue = ("64,7,2",)                           # f64 split scan at 16 envs per wave
+        queue = ("64,7,2", "64,7,3", "32,7,3")        # f64: split scan at 16 envs/wave; block-wide dynamics
     for v in ("64,7,1", "32,0,1", "32,3,1", "16,7,1", "32,7,1", "16,0,2", "32,3,2", "8,7,2", "16,7,2", "32,7,2") + queue:
         env = make(env_id, n, seed=4, precision=precision, kernel_variant=v)
         env.reset(seed=4)
@@ -403,7 +403,7 @@ def test_step_variants_bit_identical_scattered(precision):
     assert far.mean() > 0.1, far.mean()          # the far path is actually exercised
     a = torch.from_numpy(rng.uniform([0.2, -1], [1, 1], size=(n, 2)).astype(np.float32)).cuda()
     ref = None
-    queue = ("128,7,4", "128,7,5", "16,7,5") if precision == "f32" else ("64,7,2",)   # block queue: f32 only
+    queue = ("128,7,4", "128,7,5", "16,7,5") if precision == "f32" else ("64,7,2", "64,7,3", "32,7,3")
     for v in ("64,7,1", "32,3,1", "32,7,1", "16,0,1", "16,3,2", "8,7,2", "16,7,2") + queue:
         # copy=False: final_obs rows of envs that did not end keep the (identical) buffer contents
         env = make("usv-simple", n, seed=3, precision=precision, kernel_variant=v, copy=False)

@@ -472,7 +472,10 @@ def test_two_process_sharding_bit_identical():
     ("usv-simple", "f32", "128,7,5", 8192),   # the same kernel forced at a small count (ragged tail too)
     ("usv-asmc-simple", "f32", None, 8192),   # split block-queue step (kind 4)
     ("usv-simple", "f32", "16,7,2", 8192),    # split wave scan (kind 2): vm_wait<2|4>
-    ("usv-simple", "f64", None, 8192),        # fused wave kernel (kind 1)
+    ("usv-simple", "f64", None, 8192),        # f64 block-wide dynamics + wave scan (kind 3, 8 envs/wave)
+    ("usv-simple", "f64", None, 65536),       # the same at 16 envs/wave (the f64 default at C3)
+    ("usv-simple", "f64", "32,7,2", 8192),    # f64 split wave scan (kind 2)
+    ("usv-simple", "f64", "64,7,1", 8192),    # fused wave kernel (kind 1)
 ])
 def test_safe_vmcnt_build_bit_identical(env_id, precision, variant, n):
     """libusvhip_safe.so (USV_SAFE_VMCNT: every hand-counted vm_wait is vmcnt(0)) against the product

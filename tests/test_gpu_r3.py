@@ -160,7 +160,7 @@ def test_many_obstacles_variants_bit_identical(precision):
     acts = [torch.from_numpy(rng.uniform([0.2, -1], [1, 1], size=(n, 2)).astype(np.float32)).cuda()
             for _ in range(T)]
     ref = None
-    extra = ("64,7,2",) if precision == "f64" else ()     # f64 split scan at 16 envs per wave
+    extra = ("64,7,2", "64,7,3") if precision == "f64" else ()   # f64: 16 envs/wave, block-wide dynamics
     for v in ("64,7,1", "16,7,1", "32,3,1", "16,0,1", "16,7,2", "8,3,2", "32,0,2") + extra:
         env = make("usv-simple", n, seed=8, precision=precision, obstacle_cap=64, max_episode_steps=8,
                    kernel_variant=v)
@@ -192,6 +192,10 @@ def test_kernel_variant_validation():
         make("usv-simple", 64, kernel_variant="48,7,1")
     with pytest.raises(gym_usv_amd.UsvLibError):
         make("usv-asmc-v0", 64, kernel_variant="64,7,1")
+    with pytest.raises(gym_usv_amd.UsvLibError):             # block-wide dynamics: f64 usv-simple only
+        make("usv-simple", 64, kernel_variant="64,7,3")
+    with pytest.raises(gym_usv_amd.UsvLibError):
+        make("usv-asmc-simple", 64, precision="f64", kernel_variant="64,7,3")
 
 
 # --------------------------------------------------------------------------- info
