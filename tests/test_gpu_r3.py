@@ -296,3 +296,28 @@ def test_copy_semantics():
     assert torch.equal(o2[7:], last[7:]) and o2.data_ptr() != last.data_ptr()
     for e in (a, b, c):
         e.close()
+
+@pytest.mark.parametrize("n", [1, 77, 1077])
+def test_f64_block_dynamics_ragged_sizes(n):
+    """Kind 3 (f64: wave 0 of each 4-wave block runs the block's dynamics, poses handed over in LDS)
+    on env counts that leave a partial block, a partial wave and an odd last pair: bit-identical to
+    the split scan (kind 2) and the fused wave kernel (kind 1) over a rollout with resets."""
+    T = 40
+    gen = torch.Generator(device="cuda").manual_seed(15)
+    acts = [torch.rand(n, 2, device="cuda", generator=gen) * torch.tensor([0.8, 2.0], device="cuda")
+            + torch.tensor([0.2, -1.0], device="cuda") for _ in range(T)]
+    ref = None
+    for v in ("64,7,1", "64,7,3", "32,7,3", "64,7,2"):
+        env = make("usv-simple", n, seed=16, precision="f64", max_episode_steps=12, kernel_variant=v, copy=False)
+        env.reset(seed=16)
+        outs = []
+        for a in acts:
+            o, r, te, tr, info = env.step(a)
+            outs.append((o.clone(), r.clone(), te.clone(), tr.clone(), info["final_obs"].clone()))
+        env.close()
+        if ref is None:
+            ref = outs
+            continue
+        for t, (a_, b_) in enumerate(zip(ref, outs)):
+            for x, y in zip(a_, b_):
+                assert torch.equal(x, y), f"variant {v} differs at step {t} (n={n})"
