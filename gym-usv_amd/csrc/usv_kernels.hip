@@ -539,9 +539,12 @@ __device__ void env_dynamics(const State<R>& S, int e, float a_u, float a_r, flo
     const R c0 = R(a_u), c1 = R(a_r);
     // perturb_step of the episode's UsvAsmc: 2 compute() x 10 substeps per env step (usv_asmc.py:199)
     const bool pert = S.perturb != 0;
-    for (int k = 0; k < 20; ++k) {
-      if constexpr (std::is_same<R, float>::value) asmc_substep_f32(s, c0, c1, x, y, psi, u, v, r, 20 * el0 + k, pert);
-      else asmc_substep<R>(s, c0, c1, x, y, psi, u, v, r, 20 * el0 + k, pert);
+    if constexpr (std::is_same<R, float>::value) {
+      float xl = 0.0f, yl = 0.0f, pl = 0.0f;        // compensation terms of the pose (asmc_substep_f32)
+      for (int k = 0; k < 20; ++k) asmc_substep_f32(s, c0, c1, x, y, psi, u, v, r, xl, yl, pl, 20 * el0 + k, pert);
+      x += xl; y += yl; psi += pl;
+    } else {
+      for (int k = 0; k < 20; ++k) asmc_substep<R>(s, c0, c1, x, y, psi, u, v, r, 20 * el0 + k, pert);
     }
 #pragma unroll
     for (int i = 0; i < kAsmcN; ++i) S.asmc[(size_t)i * S.N + e] = s[i];

@@ -63,15 +63,15 @@ def test_golden_trajectory_replay(golden, fname, env_id, precision):
     alive = np.ones(n, bool)
     worst = {"hdr": 0.0, "rew": 0.0}
     flips, rays = 0, 0
-    # f32 trajectories accumulate rounding along the rollout (about 5x the measured worst case,
-    # r02: usv-simple header 1.4e-6 / reward 1.3e-5; usv-asmc-simple 5.2e-6 / 1.0e-4).  The ASMC
-    # reward error is two ulps of a ~50 m float32 position (ye_reward slope 1/0.075 per m) after
-    # 20 substeps per step: past SURVEY §8(c)'s single-step 1e-4, which test_single_step_parity_4096
-    # holds; DESIGN.md "Oracle and parity" records this trajectory bound.
+    # f32 trajectories accumulate rounding along the rollout (about 5x the measured worst case:
+    # usv-simple header 1.4e-6 / reward 1.3e-5; usv-asmc-simple 2.7e-6 / 3.5e-5 since the f32 ASMC
+    # integrates the pose with compensated summation -- 1.0e-4 without it, the reward's ye term
+    # amplifying a ~50 m float32 position rounded 20 times per step).  The usv-asmc-simple reward
+    # tolerance is SURVEY §8(c)'s 1e-4.
     if precision == "f64":
         hdr_tol, sens_tol, rew_tol = 2e-6, 2e-6, 1e-8
     else:
-        hdr_tol, sens_tol, rew_tol = (7e-6, 1e-4, 7e-5) if env_id == "usv-simple" else (3e-5, 1e-4, 5e-4)
+        hdr_tol, sens_tol, rew_tol = (7e-6, 1e-4, 7e-5) if env_id == "usv-simple" else (1.5e-5, 1e-4, 1e-4)
     for t in range(T):
         a = torch.from_numpy(g["actions"][:, t]).cuda()
         obs, rew, term, trunc, _ = env.step(a)
