@@ -142,7 +142,7 @@ class PPO:
             self.b_val[t] = self.model.value(self.obs)
             a_env = torch.max(torch.min(a, self.a_hi), self.a_lo)          # SB3 clips Box actions
             obs, rew, term, trunc, info = self.env.step(a_env)
-            done = term | trunc
+            done = info["_final_obs"]                                     # terminated | truncated
             self.abs_ye.append(obs[:, 5].abs().mean() * 10.0)   # obs[5] = ye / 10 (simple_env.py:79-80)
             nxt, term_rows = self.stack.step(obs, done, info["final_obs"])
             r = rew.float().clone()

@@ -88,6 +88,7 @@ template <typename R> struct IO {
   const uint8_t* mask;     // [N] or null (reset kernel)
   R* info;                 // [N][USV_INFO_DIM] in R (f32 / f64 build) or null: step info (step kernels) / reset info
   int kpath;               // reset kernel: options['place_obstacles_on_path'] (0 = none)
+  uint8_t* done;           // [N] terminated | truncated (gymnasium's info['_final_obs']) or null
 };
 
 constexpr int kBlock = 256;
@@ -1465,6 +1466,7 @@ __device__ __forceinline__ void scan_epilogue(const State<R>& S, const IO<R>& io
     else if (coll) io.rew[e] = R(-20) + io.rew[e];
     io.term[e] = (term_m >> l) & 1;
     if (have_partial) io.trunc[e] = (trunc_m >> l) & 1;
+    if (io.done) io.done[e] = ((term_m | trunc_m) >> l) & 1;
   }
   if (S.autoreset == USV_AUTORESET_SAME_STEP) {
     for (int k = 0; k < ne; ++k)
@@ -1920,7 +1922,9 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
       const bool coll_l = hb ? collB : collA;           // 32..63 env B
       st_out(io.rew + el, coll_l ? -20.0f + meta.x : meta.x);
       io.term[el] = term_l;
-      const unsigned long long dm = ballot(term_l | ((nt >> 16) & 1));
+      const bool done_l = term_l | ((nt >> 16) & 1);
+      if (io.done) io.done[el] = done_l;               // (wave-uniform branch; >= 7 stores still follow the DMA)
+      const unsigned long long dm = ballot(done_l);
       const bool doneA = (unsigned)dm != 0u, doneB = hasB && (unsigned)(dm >> 32) != 0u;
       if (doneA | doneB) {
         if (doneA) q_emit_done(S, io, e0, sa, recs + k0 * kQRec);
@@ -2238,6 +2242,7 @@ __global__ __launch_bounds__(kBlock) void v0_step_kernel(State<R> S, IO<R> io) {
   io.rew[e] = done ? R(-1) : (pa < R(kPi / 2) ? r_act + r_ye : r_ak);
   io.term[e] = done;
   io.trunc[e] = trunc;
+  if (io.done) io.done[e] = done | trunc;
   float* row = io.obs + (size_t)e * 6;
   // stored state (float32, :247-251)
   S.F(F_U)[e] = q32(u); S.F(F_V)[e] = q32(v); S.F(F_R)[e] = q32(r);
@@ -2385,6 +2390,7 @@ __global__ __launch_bounds__(kBlock) void legacy_step_kernel(State<R> S, IO<R> i
   io.rew[e] = done ? R(-1) : reward;
   io.term[e] = done;
   io.trunc[e] = trunc;
+  if (io.done) io.done[e] = done | trunc;
   S.F(F_U)[e] = u; S.F(F_V)[e] = v; S.F(F_R)[e] = r;                             // :247-251
   S.F(F_X)[e] = x; S.F(F_Y)[e] = y; S.F(F_PSI)[e] = psi;
   S.V(kV0Aux)[e] = e_u_int; S.V(kV0Aux + 1)[e] = ka_u; S.V(kV0Aux + 2)[e] = ka_psi;
@@ -2571,13 +2577,13 @@ void* pick_q(int mode, bool fused, bool small = false) {
 
 template <typename R>
 int launch_step_kernels(Handle* h, State<R>& S, const float* act, float* obs, void* rew, uint8_t* term,
-                        uint8_t* trunc, float* fobs, void* info, hipStream_t st);
+                        uint8_t* trunc, uint8_t* done, float* fobs, void* info, hipStream_t st);
 
 // The step, then (NumPy-exact reset mode) the resets of the envs that ended in it.
 template <typename R>
 int launch_step(Handle* h, State<R>& S, const float* act, float* obs, void* rew, uint8_t* term,
-                uint8_t* trunc, float* fobs, void* info, hipStream_t st) {
-  const int rc = launch_step_kernels(h, S, act, obs, rew, term, trunc, fobs, info, st);
+                uint8_t* trunc, uint8_t* done, float* fobs, void* info, hipStream_t st) {
+  const int rc = launch_step_kernels(h, S, act, obs, rew, term, trunc, done, fobs, info, st);
   // (the legacy kernels reset inline, from the MT19937 state, in the NumPy-exact mode too)
   if (rc != USV_OK || S.autoreset != USV_AUTORESET_SAME_STEP || is_legacy(h->cfg.mode)) return rc;
   IO<R> io{act, obs, (R*)rew, term, trunc, fobs, nullptr, nullptr, 0};
@@ -2597,8 +2603,8 @@ int launch_step(Handle* h, State<R>& S, const float* act, float* obs, void* rew,
 
 template <typename R>
 int launch_step_kernels(Handle* h, State<R>& S, const float* act, float* obs, void* rew, uint8_t* term,
-                        uint8_t* trunc, float* fobs, void* info, hipStream_t st) {
-  IO<R> io{act, obs, (R*)rew, term, trunc, fobs, nullptr, is_legacy(h->cfg.mode) ? nullptr : (R*)info, 0};
+                        uint8_t* trunc, uint8_t* done, float* fobs, void* info, hipStream_t st) {
+  IO<R> io{act, obs, (R*)rew, term, trunc, fobs, nullptr, is_legacy(h->cfg.mode) ? nullptr : (R*)info, 0, done};
   if (is_legacy(h->cfg.mode)) {
     const dim3 grid((S.N + kBlock - 1) / kBlock), block(kBlock);
     if (h->cfg.mode == USV_MODE_ASMC_V0)
@@ -3030,18 +3036,19 @@ int usv_reset(void* hp, const uint8_t* mask, float* obs, void* stream) {
 }
 
 int usv_step_ex(void* hp, const float* act, float* obs, void* rew, uint8_t* term, uint8_t* trunc,
-                float* fobs, void* info, void* stream) {
+                uint8_t* done, float* fobs, void* info, void* stream) {
   Handle* h = as_handle(hp);
   if (!h || !act || !obs || !rew || !term || !trunc) return fail(USV_ERR_ARG, "null argument");
   DeviceGuard g(h->device);
   hipStream_t st = (hipStream_t)stream;
-  return h->cfg.precision == USV_F32 ? launch_step<float>(h, h->sf, act, obs, rew, term, trunc, fobs, info, st)
-                                     : launch_step<double>(h, h->sd, act, obs, rew, term, trunc, fobs, info, st);
+  return h->cfg.precision == USV_F32
+             ? launch_step<float>(h, h->sf, act, obs, rew, term, trunc, done, fobs, info, st)
+             : launch_step<double>(h, h->sd, act, obs, rew, term, trunc, done, fobs, info, st);
 }
 
 int usv_step(void* hp, const float* act, float* obs, void* rew, uint8_t* term, uint8_t* trunc,
              float* fobs, void* stream) {
-  return usv_step_ex(hp, act, obs, rew, term, trunc, fobs, nullptr, stream);
+  return usv_step_ex(hp, act, obs, rew, term, trunc, nullptr, fobs, nullptr, stream);
 }
 
 int usv_set_experiment(void* hp, const usv_experiment* x) {

@@ -14,7 +14,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 # diagnostic builds (tools/) may point at another in-tree copy of the library
 LIB_PATH = os.environ.get("USV_LIB_PATH", LIB_PATH)
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 MODE_SIMPLE, MODE_ASMC_SIMPLE, MODE_ASMC_V0, MODE_ASMC_YE_INT_V0, MODE_PID_V0 = 0, 1, 2, 3, 4
 F32, F64 = 0, 1
 AUTORESET_SAME_STEP, AUTORESET_DISABLED = 0, 1
@@ -73,7 +73,7 @@ SIGNATURES = [
     ("usv_reset_ex", ctypes.c_int, [_vp, _vp, _vp, ctypes.POINTER(UsvResetOptions), _vp, _vp]),
     ("usv_set_experiment", ctypes.c_int, [_vp, ctypes.POINTER(UsvExperiment)]),
     ("usv_step", ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
-    ("usv_step_ex", ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    ("usv_step_ex", ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     ("usv_field_info", ctypes.c_int, [_vp, _i32, ctypes.POINTER(_i32), ctypes.POINTER(_i32),
                                       ctypes.POINTER(ctypes.c_char_p)]),
     ("usv_get_field", ctypes.c_int, [_vp, _i32, _vp, _sz]),

@@ -129,7 +129,7 @@ class Sb3VecEnv:
     def step_wait(self):
         a = torch.as_tensor(np.asarray(self._actions, dtype=np.float32), device=self.venv.device)
         obs, rew, term, trunc, info = self.venv.step(a)
-        done = term | trunc
+        done = info["_final_obs"]                       # terminated | truncated, written by the step kernel
         self._ep_ret += rew.to(torch.float64)
         self._ep_len += 1
         final = info.get("final_obs")

@@ -136,6 +136,7 @@ class UsvVectorEnv:
         self.reward = torch.zeros(n, dtype=rdt, **kw)
         self._term = torch.zeros(n, dtype=torch.uint8, **kw)
         self._trunc = torch.zeros(n, dtype=torch.uint8, **kw)
+        self._done = torch.zeros(n, dtype=torch.uint8, **kw)   # terminated | truncated, written by the step kernel
         self.max_episode_steps = cfg.max_episode_steps
         self.single_observation_space, self.single_action_space = _spaces(env_id)
         self._fields = self._field_table()
@@ -150,8 +151,9 @@ class UsvVectorEnv:
         self.info_buf = torch.zeros((n, _lib.INFO_DIM), dtype=rdt, **kw) if self.info_enabled else None
         # step() hot path: the persistent buffers' pointers and bool views, made once
         self._out_ptrs = (_ptr(self.obs), _ptr(self.reward), _ptr(self._term), _ptr(self._trunc),
-                          _ptr(self.final_obs), _ptr(self.info_buf))
+                          _ptr(self._done), _ptr(self.final_obs), _ptr(self.info_buf))
         self._term_b, self._trunc_b = self._term.view(torch.bool), self._trunc.view(torch.bool)
+        self._done_b = self._done.view(torch.bool)
         self._last_obs = self.obs              # the latest obs rows (a masked reset keeps the others)
         self._last_rew = self.reward
         self.options = dict(options or {})
@@ -276,19 +278,20 @@ class UsvVectorEnv:
             obs = torch.empty((n, self.obs_dim), dtype=torch.float32, device=dev)
             fobs = torch.empty((n, self.obs_dim), dtype=torch.float32, device=dev)
             rew = torch.empty(n, dtype=self._rdt, device=dev)
-            flags = torch.empty((2, n), dtype=torch.bool, device=dev)
-            term, trunc = flags[0], flags[1]
+            flags = torch.empty((3, n), dtype=torch.bool, device=dev)
+            term, trunc, done = flags[0], flags[1], flags[2]
             ib = torch.empty_like(self.info_buf) if self.info_enabled else None
-            ptrs = (_ptr(obs), _ptr(rew), _ptr(term), _ptr(trunc), _ptr(fobs), _ptr(ib))
+            ptrs = (_ptr(obs), _ptr(rew), _ptr(term), _ptr(trunc), _ptr(done), _ptr(fobs), _ptr(ib))
         else:
             obs, rew, fobs, ib = self.obs, self.reward, self.final_obs, self.info_buf
-            term, trunc = self._term_b, self._trunc_b
+            term, trunc, done = self._term_b, self._trunc_b, self._done_b
             ptrs = self._out_ptrs
-        o, r, te, tr, fo, inf = ptrs
-        self._check(self.lib.usv_step_ex(self._h, ctypes.c_void_p(a.data_ptr()), o, r, te, tr, fo, inf,
+        o, r, te, tr, dn, fo, inf = ptrs
+        # the kernel also writes the done mask (terminated | truncated): no extra launch per step
+        self._check(self.lib.usv_step_ex(self._h, ctypes.c_void_p(a.data_ptr()), o, r, te, tr, dn, fo, inf,
                                         _stream_ptr(self.device)))
         self._last_obs, self._last_rew = obs, rew
-        info = {"final_obs": fobs, "_final_obs": term | trunc}
+        info = {"final_obs": fobs, "_final_obs": done}
         if self.info_enabled:
             self.info_buf = ib
             info.update(self._info_dict(ib, rew))

@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define USV_ABI_VERSION 3
+#define USV_ABI_VERSION 4
 #define USV_SENSOR_COUNT 128
 #define USV_OBS_DIM 143      /* 15 + 128, simple_env.py:27 */
 #define USV_ACT_DIM 2        /* simple_env.py:30 */
@@ -232,12 +232,13 @@ int usv_set_experiment(void* handle, const usv_experiment* experiment);
  *                 (rows of envs not done are left untouched). */
 int usv_step(void* handle, const float* act_dev, float* obs_dev, void* rew_dev,
              uint8_t* term_dev, uint8_t* trunc_dev, float* final_obs_dev, void* stream);
-/* usv_step that also writes the per-step info rows into info_dev [num_envs][USV_INFO_DIM] f32 / f64
- * by precision (usv-simple / usv-asmc-simple; the legacy *-v0 ids return {} in the reference and
- * ignore it). */
+/* usv_step with two optional outputs (NULL = not written):
+ *   done_dev  [num_envs] u8: terminated | truncated, i.e. gymnasium's info['_final_obs'] mask (ABI v4)
+ *   info_dev  [num_envs][USV_INFO_DIM] f32 / f64 by precision: the per-step info rows (usv-simple /
+ *             usv-asmc-simple; the legacy *-v0 ids return {} in the reference and ignore it). */
 int usv_step_ex(void* handle, const float* act_dev, float* obs_dev, void* rew_dev,
-                uint8_t* term_dev, uint8_t* trunc_dev, float* final_obs_dev, void* info_dev,
-                void* stream);
+                uint8_t* term_dev, uint8_t* trunc_dev, uint8_t* done_dev, float* final_obs_dev,
+                void* info_dev, void* stream);
 
 /* Select the step-kernel variant of a usv-simple / usv-asmc-simple handle (verification and
  * tuning: every variant computes bit-identical outputs, tests/test_gpu_*.py compare them bitwise).

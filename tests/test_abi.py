@@ -70,7 +70,7 @@ def test_create_rejects_bad_config_without_gpu(lib):
     # null handles are reported, not dereferenced
     assert lib.usv_step(None, None, None, None, None, None, None, None) == -1
     assert lib.usv_reset(None, None, None, None) == -1
-    assert lib.usv_step_ex(None, None, None, None, None, None, None, None, None) == -1
+    assert lib.usv_step_ex(None, None, None, None, None, None, None, None, None, None) == -1
     assert lib.usv_reset_ex(None, None, None, None, None, None) == -1
     assert lib.usv_set_experiment(None, None) == -1
     cfg.abi_version = _lib.ABI_VERSION

@@ -321,3 +321,35 @@ def test_f64_block_dynamics_ragged_sizes(n):
         for t, (a_, b_) in enumerate(zip(ref, outs)):
             for x, y in zip(a_, b_):
                 assert torch.equal(x, y), f"variant {v} differs at step {t} (n={n})"
+
+
+@pytest.mark.parametrize("env_id,precision,variant", [
+    ("usv-simple", "f32", None), ("usv-simple", "f32", "16,7,5"), ("usv-simple", "f32", "128,7,4"),
+    ("usv-simple", "f32", "16,7,2"), ("usv-simple", "f32", "64,7,1"), ("usv-simple", "f64", None),
+    ("usv-simple", "f64", "32,7,2"), ("usv-asmc-simple", "f32", None), ("usv-asmc-v0", "f32", None),
+    ("usv-pid-v0", "f64", None), ("usv-asmc-ye-int-v0", "f32", None)])
+def test_done_mask_written_by_kernel(env_id, precision, variant):
+    """info['_final_obs'] is written by the step kernel itself (ABI v4 done output, no extra launch):
+    equal to terminated | truncated on every step of a rollout with resets, for every kernel kind,
+    both output modes."""
+    n, T = 1000, 30
+    gen = torch.Generator(device="cuda").manual_seed(31)
+    legacy = env_id in ("usv-asmc-v0", "usv-pid-v0", "usv-asmc-ye-int-v0")
+    ad = 1 if legacy else 2
+    for copy in (True, False):
+        kw = {} if variant is None else {"kernel_variant": variant}
+        if not legacy:
+            kw["max_episode_steps"] = 9
+        env = make(env_id, n, seed=32, precision=precision, copy=copy, **kw)
+        env.reset(seed=32)
+        ends = 0
+        for _ in range(T):
+            a = torch.rand(n, ad, device="cuda", generator=gen) * 2 - 1
+            if not legacy:
+                a[:, 0] = a[:, 0].abs() * 0.8 + 0.2
+            o, r, te, tr, info = env.step(a)
+            m = info["_final_obs"]
+            assert m.dtype == torch.bool and torch.equal(m, te | tr)
+            ends += int(m.sum())
+        env.close()
+        assert ends > 0 or legacy          # (the legacy ids have no TimeLimit: episodes may outlast T)

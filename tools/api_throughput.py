@@ -1,7 +1,8 @@
 """Env-steps/s at one env count through the three host surfaces (config C2/C5 scale):
 
 * ``step_raw``  -- the C-ABI launch into caller-owned buffers (what bench.py times);
-* ``step``      -- the public UsvVectorEnv.step (torch.as_tensor / dtype / shape checks, outputs in HBM);
+* ``step``      -- the public UsvVectorEnv.step (torch.as_tensor / dtype / shape checks, outputs in HBM;
+                   fresh tensors), ``step_nocopy`` the same with copy=False (persistent buffers);
 * ``sb3``       -- Sb3VecEnv.step (VecFrameStack(5) on device, NumPy host copies + Monitor infos per
                    step, i.e. what an SB3 algorithm consumes).
 
@@ -50,7 +51,11 @@ def main():
     te, tr = torch.empty(n, dtype=torch.uint8, device="cuda"), torch.empty(n, dtype=torch.uint8, device="cuda")
     out = {"env_id": a.env_id, "envs": n, "steps": a.steps}
     out["step_raw"] = rate(lambda k: env.step_raw(acts[k % 64], obs, rew, te, tr, fobs), a.steps, n)
-    out["step"] = rate(lambda k: env.step(acts[k % 64]), a.steps, n)
+    out["step"] = rate(lambda k: env.step(acts[k % 64]), a.steps, n)               # copy=True (default)
+    env.close()
+    env = gym_usv_amd.make_vec(a.env_id, n, seed=0, copy=False)
+    env.reset(seed=0)
+    out["step_nocopy"] = rate(lambda k: env.step(acts[k % 64]), a.steps, n)        # persistent buffers
     env.close()
     sb = gym_usv_amd.make_sb3_vec_env(a.env_id, n, frame_stack=5, seed=0)
     sb.reset()
