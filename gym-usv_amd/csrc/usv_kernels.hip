@@ -2552,7 +2552,7 @@ void* pick_scan_lid(int lid) {
     if (lid == 3) return (void*)&scan_kernel_tight<R, MODE, EPW, 3, WPB>;
     return (void*)&scan_kernel_tight<R, MODE, EPW, 7, WPB>;
   }
-  if constexpr (std::is_same<R, double>::value && MODE == USV_MODE_SIMPLE) {
+  if constexpr (std::is_same<R, double>::value) {
     if (lid == 7) return (void*)&scan_kernel_d<R, MODE, EPW, 7, WPB>;
   }
   if (lid == 0) return (void*)&scan_kernel<R, MODE, EPW, 0, WPB>;
@@ -2563,7 +2563,7 @@ template <typename R, int MODE, int WPB>
 void* pick_scan(int epw, int lid) {
   if (epw == 2) return pick_scan_lid<R, MODE, 2, WPB>(lid);
   if (epw == 8) return pick_scan_lid<R, MODE, 8, WPB>(lid);
-  if constexpr (std::is_same<R, double>::value && MODE == USV_MODE_SIMPLE && WPB == 4)
+  if constexpr (std::is_same<R, double>::value && WPB == 4)
     if (epw == 16) return pick_scan_lid<R, MODE, 16, WPB>(lid);   // f64: one round of waves at 65 536 envs
   return pick_scan_lid<R, MODE, 4, WPB>(lid);
 }
@@ -2928,7 +2928,13 @@ int usv_create(const usv_config* cfg, int32_t device, void** out) {
   if (cfg->mode == USV_MODE_ASMC_SIMPLE) {
     // ASMC's 20 substeps want full-width dynamics: a separate dyn_kernel, then the block queue
     // (45.7 us vs 46.7 for the split wave scan at 65 536 envs)
-    if (queue) { h->kind = 4; h->epb = kQE; } else { h->kind = 2; h->epb = 16; }
+    // f64 (window lidar, cap <= 32): the split f64 wave scan at 16 envs/wave from 49 152 envs
+    // (72.0 us at 65 536 envs against 77.4 at 4); block-wide dynamics (kind 3) spill the f64 ASMC
+    // state at 4 waves per SIMD (94 us)
+    const bool f64w = cfg->precision == USV_F64 && cfg->lidar_algo == USV_LIDAR_WINDOW && cfg->obstacle_cap <= 32;
+    if (queue) { h->kind = 4; h->epb = kQE; }
+    else if (f64w) { h->kind = 2; h->epb = cfg->num_envs >= 49152 ? 64 : 32; }
+    else { h->kind = 2; h->epb = 16; }
   } else if (queue) {
     h->kind = 5;                        // block-queue step: 16-wave blocks of 128 envs, or 8-wave blocks
     h->epb = cfg->num_envs < kQSmallBelow ? kQE_S : kQE;   // of 16 below kQSmallBelow envs
@@ -2958,7 +2964,7 @@ int usv_set_kernel_variant(void* hp, int32_t kind, int32_t epb, int32_t lid) {
   const bool lid_ok = lid == 0 || lid == 3 || lid == 7;
   const bool wave_ok = kind == 1 && (epb == 16 || epb == 32 || epb == 64) && lid_ok;
   const bool split_ok = kind == 2 && (epb == 8 || epb == 16 || epb == 32 ||
-                                      (epb == 64 && lid == 7 && cfg->precision == USV_F64 && cfg->mode == USV_MODE_SIMPLE)) && lid_ok;
+                                      (epb == 64 && lid == 7 && cfg->precision == USV_F64)) && lid_ok;
   const bool blockdyn_ok = kind == 3 && (epb == 32 || epb == 64) && lid == 7 && cfg->precision == USV_F64 &&
                            cfg->mode == USV_MODE_SIMPLE;
   const bool queue_ok = (kind == 4 || kind == 5) && (epb == kQE || (kind == 5 && epb == kQE_S)) && lid == 7 &&

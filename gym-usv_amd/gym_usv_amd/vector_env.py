@@ -278,8 +278,7 @@ class UsvVectorEnv:
             obs = torch.empty((n, self.obs_dim), dtype=torch.float32, device=dev)
             fobs = torch.empty((n, self.obs_dim), dtype=torch.float32, device=dev)
             rew = torch.empty(n, dtype=self._rdt, device=dev)
-            flags = torch.empty((3, n), dtype=torch.bool, device=dev)
-            term, trunc, done = flags[0], flags[1], flags[2]
+            term, trunc, done = torch.empty((3, n), dtype=torch.bool, device=dev).unbind(0)
             ib = torch.empty_like(self.info_buf) if self.info_enabled else None
             ptrs = (_ptr(obs), _ptr(rew), _ptr(term), _ptr(trunc), _ptr(done), _ptr(fobs), _ptr(ib))
         else:

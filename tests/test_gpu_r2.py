@@ -476,6 +476,7 @@ def test_two_process_sharding_bit_identical():
     ("usv-simple", "f64", None, 65536),       # the same at 16 envs/wave (the f64 default at C3)
     ("usv-simple", "f64", "32,7,2", 8192),    # f64 split wave scan (kind 2)
     ("usv-simple", "f64", "64,7,1", 8192),    # fused wave kernel (kind 1)
+    ("usv-asmc-simple", "f64", None, 65536),  # f64 ASMC: split f64 wave scan at 16 envs/wave (kind 2)
 ])
 def test_safe_vmcnt_build_bit_identical(env_id, precision, variant, n):
     """libusvhip_safe.so (USV_SAFE_VMCNT: every hand-counted vm_wait is vmcnt(0)) against the product
