@@ -1769,7 +1769,10 @@ template <int QE = kQE, int QW = kQW> __host__ __device__ constexpr size_t lds_q
 static_assert(2 * lds_q_bytes() <= 160 * 1024, "two blocks per CU");
 static_assert(4 * lds_q_bytes<kQE_S, kQW_S>() <= 160 * 1024, "four small blocks per CU");
 
-template <int MODE, bool FUSED, int kQE = ::usv::kQE, int kQW = ::usv::kQW>
+// DONE: also write the done mask (io.done, ABI v4).  A template switch rather than a runtime test:
+// the raw step (usv_step, io.done null) then carries neither the pointer nor its branch in the pair
+// loop, whose SGPR budget is at its limit (a runtime test cost 0.25 us per launch).
+template <int MODE, bool FUSED, bool DONE = false, int kQE = ::usv::kQE, int kQW = ::usv::kQW>
 __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<float>& io) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
@@ -1923,7 +1926,7 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
       st_out(io.rew + el, coll_l ? -20.0f + meta.x : meta.x);
       io.term[el] = term_l;
       const bool done_l = term_l | ((nt >> 16) & 1);
-      if (io.done) io.done[el] = done_l;               // (wave-uniform branch; >= 7 stores still follow the DMA)
+      if constexpr (DONE) io.done[el] = done_l;        // (>= 7 stores still follow the DMA)
       const unsigned long long dm = ballot(done_l);
       const bool doneA = (unsigned)dm != 0u, doneB = hasB && (unsigned)(dm >> 32) != 0u;
       if (doneA | doneB) {
@@ -1962,15 +1965,15 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
   USV_STAMP_W(6);
 }
 
-template <int MODE, bool FUSED>
+template <int MODE, bool FUSED, bool DONE>
 __global__ __launch_bounds__(kQW * kWave) __attribute__((amdgpu_num_sgpr(USV_QSGPR), amdgpu_waves_per_eu(USV_QWPE, USV_QWPE)))
-void step_q_kernel(State<float> S, IO<float> io) { step_q_body<MODE, FUSED>(S, io); }
-template <int MODE>
+void step_q_kernel(State<float> S, IO<float> io) { step_q_body<MODE, FUSED, DONE>(S, io); }
+template <int MODE, bool DONE>
 __global__ __launch_bounds__(kQW_S * kWave) __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8)))
-void step_qs_kernel(State<float> S, IO<float> io) { step_q_body<MODE, true, kQE_S, kQW_S>(S, io); }
+void step_qs_kernel(State<float> S, IO<float> io) { step_q_body<MODE, true, DONE, kQE_S, kQW_S>(S, io); }
 
 // Split block-queue step, first half: full-width lane-per-env dynamics writing the env records
-// (make_qrec) for step_q_kernel<MODE, false>, plus truncated and the info row.
+// (make_qrec) for step_q_kernel<MODE, false, DONE>, plus truncated and the info row.
 template <int MODE>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 2))) void dyn_rec_kernel(State<float> S, IO<float> io) {
   const int e = blockIdx.x * kBlock + threadIdx.x;
@@ -2568,11 +2571,16 @@ void* pick_scan(int epw, int lid) {
   return pick_scan_lid<R, MODE, 4, WPB>(lid);
 }
 
-void* pick_q(int mode, bool fused, bool small = false) {
+template <bool DONE>
+void* pick_q_done(int mode, bool fused, bool small) {
   const bool simple = mode == USV_MODE_SIMPLE;
-  if (small) return simple ? (void*)&step_qs_kernel<USV_MODE_SIMPLE> : (void*)&step_qs_kernel<USV_MODE_ASMC_SIMPLE>;
-  if (fused) return simple ? (void*)&step_q_kernel<USV_MODE_SIMPLE, true> : (void*)&step_q_kernel<USV_MODE_ASMC_SIMPLE, true>;
-  return simple ? (void*)&step_q_kernel<USV_MODE_SIMPLE, false> : (void*)&step_q_kernel<USV_MODE_ASMC_SIMPLE, false>;
+  if (small) return simple ? (void*)&step_qs_kernel<USV_MODE_SIMPLE, DONE> : (void*)&step_qs_kernel<USV_MODE_ASMC_SIMPLE, DONE>;
+  if (fused) return simple ? (void*)&step_q_kernel<USV_MODE_SIMPLE, true, DONE>
+                           : (void*)&step_q_kernel<USV_MODE_ASMC_SIMPLE, true, DONE>;
+  return simple ? (void*)&step_q_kernel<USV_MODE_SIMPLE, false, DONE> : (void*)&step_q_kernel<USV_MODE_ASMC_SIMPLE, false, DONE>;
+}
+void* pick_q(int mode, bool fused, bool small = false, bool done = false) {
+  return done ? pick_q_done<true>(mode, fused, small) : pick_q_done<false>(mode, fused, small);
 }
 
 template <typename R>
@@ -2627,7 +2635,7 @@ int launch_step_kernels(Handle* h, State<R>& S, const float* act, float* obs, vo
       }
       const bool small = h->kind == 5 && h->epb == kQE_S;
       const int qe = small ? kQE_S : kQE, qw = small ? kQW_S : kQW;
-      HIP_TRY(hipLaunchKernel(pick_q(h->cfg.mode, h->kind == 5, small), dim3((S.N + qe - 1) / qe), dim3(qw * kWave),
+      HIP_TRY(hipLaunchKernel(pick_q(h->cfg.mode, h->kind == 5, small, io.done != nullptr), dim3((S.N + qe - 1) / qe), dim3(qw * kWave),
                               args, small ? lds_q_bytes<kQE_S, kQW_S>() : lds_q_bytes(), st));
       return USV_OK;
     }
@@ -2840,11 +2848,13 @@ int set_experiment(Handle* h, State<R>& S, const usv_experiment* x) {
 // The block-queue step's LDS exceeds the 64 KiB default: raise the kernels' dynamic-LDS limit.
 int queue_lds_attr(const Handle* h) {
   if (h->kind != 4 && h->kind != 5) return USV_OK;
-  HIP_TRY(hipFuncSetAttribute(pick_q(h->cfg.mode, h->kind == 5), hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds_q_bytes()));
-  if (h->kind == 5)
-    HIP_TRY(hipFuncSetAttribute(pick_q(h->cfg.mode, true, true), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                (int)lds_q_bytes<kQE_S, kQW_S>()));
+  for (const bool done : {false, true}) {
+    HIP_TRY(hipFuncSetAttribute(pick_q(h->cfg.mode, h->kind == 5, false, done),
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_q_bytes()));
+    if (h->kind == 5)
+      HIP_TRY(hipFuncSetAttribute(pick_q(h->cfg.mode, true, true, done), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds_q_bytes<kQE_S, kQW_S>()));
+  }
   return USV_OK;
 }
 
