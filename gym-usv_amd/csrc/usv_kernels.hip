@@ -849,6 +849,25 @@ __device__ __forceinline__ int wave_incl_max_asm(int v) {
   return v;
 }
 
+// Two independent max-scans interleaved in one asm block: each DPP read of a VGPR the previous
+// VALU wrote needs two wait states, here the other chain's instruction plus one s_nop 0.
+__device__ __forceinline__ void wave_incl_max2_asm(int& a, int& b) {
+  asm volatile("s_nop 1\n\t"
+               "v_max_i32_dpp %0, %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+               "v_max_i32_dpp %1, %1, %1 row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\ts_nop 0\n\t"
+               "v_max_i32_dpp %0, %0, %0 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+               "v_max_i32_dpp %1, %1, %1 row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\ts_nop 0\n\t"
+               "v_max_i32_dpp %0, %0, %0 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+               "v_max_i32_dpp %1, %1, %1 row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\ts_nop 0\n\t"
+               "v_max_i32_dpp %0, %0, %0 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\t"
+               "v_max_i32_dpp %1, %1, %1 row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1\n\ts_nop 0\n\t"
+               "v_max_i32_dpp %0, %0, %0 row_bcast:15 row_mask:0xa bank_mask:0xf\n\t"
+               "v_max_i32_dpp %1, %1, %1 row_bcast:15 row_mask:0xa bank_mask:0xf\n\ts_nop 0\n\t"
+               "v_max_i32_dpp %0, %0, %0 row_bcast:31 row_mask:0xc bank_mask:0xf\n\t"
+               "v_max_i32_dpp %1, %1, %1 row_bcast:31 row_mask:0xc bank_mask:0xf"
+               : "+v"(a), "+v"(b));
+}
+
 template <bool RANGE_CHECK, typename Row>
 __device__ __forceinline__ void lidar_window(float dx, float dy, float key, float d, float rr, bool valid,
                                              float px, float py, float sp, float cp, const WinLds& L,
@@ -940,7 +959,7 @@ __device__ __forceinline__ void lidar_window(float dx, float dy, float key, floa
 // `far` (wave-uniform): some obstacle is >= 99 m away, where the reference's `< max range` test
 // (usv_asmc_ca_env.py:458) can matter; it is applied to every pair then.
 __device__ __forceinline__ void lidar_window2(float dx, float dy, float key, float d, float rr, bool valid, bool far,
-                                              float c0r, float s0r, float4* rec, const WinLds& L,
+                                              float c0r, float s0r, float4* rec, const WinLds& L, int* mark2,
                                               Scan<float>& A, Scan<float>& B, QProf* qp = nullptr) {
   const int l = lane_id();
   float a, b;
@@ -978,13 +997,8 @@ __device__ __forceinline__ void lidar_window2(float dx, float dy, float key, flo
   int* const mslot = L.mark + (off & (kWave - 1));
   int carry = 0;
   QMARK(2);
-  for (int base = 0, pass = 0; base < W; base += kWave, ++pass) {   // wave-uniform pass count
-    QCOUNT(9, 1);
-    if (mpass == pass) *mslot = mk0;
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");   // marks and records visible
-    __builtin_amdgcn_wave_barrier();
-    const int mk = max(wave_incl_max_asm(L.mark[l]), carry);
-    carry = __builtin_amdgcn_readlane(mk, 63);
+  // pair q = base + l of a pass whose max-scanned mark is mk: owner, ray, exact test, ds_min
+  auto pair = [&](int base, int mk) {
     const int jj = mk >> 16;                          // owner obstacle lane
     // slot of (owner env, ray) of pair q = base + l: q + (mk & 0xffff) - 32768, of which only the
     // low 8 bits are used (= those of q + mk); exact for q < W, other lanes (no hit) read some
@@ -1004,6 +1018,37 @@ __device__ __forceinline__ void lidar_window2(float dx, float dy, float key, flo
     const bool hit = (l < W - base) & (proj >= 0.0f) & (delta >= 0.0f) & (!far | (dist < (float)kSensorMax));  // :458
     if (hit)                                          // slots: env A's rays, then env B's
       atomicMin(sl, ((unsigned long long)kb << 32) | __float_as_uint(dist));
+  };
+  int base = 0, pass = 0;
+  if (W > kWave) {
+    // passes 0 and 1 at once (1.65 passes per env pair on average at C3): pass 1's marks go to mark2, 64 ints
+    // that no DMA touches (the tail of the row buffer the next pair's 768 B of rows land in; it
+    // held records last time, so it is cleared first -- LDS ops of a wave complete in order),
+    // and the two max-scans run interleaved; pass 1's carry is pass 0's last mark (18.88 -> 18.70 us
+    // per step at 65 536 envs, tools/exp_step_ab.sh)
+    QCOUNT(9, 2);
+    mark2[l] = 0;
+    if (mpass == 0) *mslot = mk0;
+    if (mpass == 1) mark2[off & (kWave - 1)] = mk0;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");   // marks and records visible
+    __builtin_amdgcn_wave_barrier();
+    int m0 = L.mark[l], m1 = mark2[l];
+    wave_incl_max2_asm(m0, m1);
+    m1 = max(m1, __builtin_amdgcn_readlane(m0, 63));
+    carry = __builtin_amdgcn_readlane(m1, 63);
+    pair(0, m0);
+    pair(kWave, m1);
+    base = 2 * kWave;
+    pass = 2;
+  }
+  for (; base < W; base += kWave, ++pass) {           // wave-uniform pass count
+    QCOUNT(9, 1);
+    if (mpass == pass) *mslot = mk0;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");   // marks and records visible
+    __builtin_amdgcn_wave_barrier();
+    const int mk = max(wave_incl_max_asm(L.mark[l]), carry);
+    carry = __builtin_amdgcn_readlane(mk, 63);
+    pair(base, mk);
   }
   QMARK(3);
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");     // all lanes' ds_min_u64 landed
@@ -1025,7 +1070,8 @@ __device__ __forceinline__ void lidar_window2(float dx, float dy, float key, flo
 // (px, py), ray-0 direction (c0r, s0r) and obstacle count nl (0: no env in this half).
 __device__ __forceinline__ void lidar_wave2(float* rows, int os, int nl, float px, float py, float c0r,
                                             float s0r, const float2* rayoff, unsigned long long* slot,
-                                            int* mark, Scan<float>& A, Scan<float>& B, QProf* qp = nullptr) {
+                                            int* mark, int* mark2, Scan<float>& A, Scan<float>& B,
+                                            QProf* qp = nullptr) {
   const int l = lane_id();
   const int jl = l & 31;
   const bool valid = jl < nl;
@@ -1043,7 +1089,8 @@ __device__ __forceinline__ void lidar_wave2(float* rows, int os, int nl, float p
   A.term = (unsigned)tb != 0u; B.term = (unsigned)(tb >> 32) != 0u;
   A.far = B.far = false;
   const bool far = (vm & ballot(d >= (float)(0.99 * kSensorMax))) != 0;
-  lidar_window2(dx, dy, key, d, rr, valid, far, c0r, s0r, reinterpret_cast<float4*>(rows), WinLds{slot, mark, rayoff}, A, B, qp);
+  lidar_window2(dx, dy, key, d, rr, valid, far, c0r, s0r, reinterpret_cast<float4*>(rows), WinLds{slot, mark, rayoff},
+                mark2, A, B, qp);
 }
 
 // Angular-window lidar for the f64 build (one env per wave).  The ray windows are sized in float from
@@ -1427,8 +1474,11 @@ __device__ __forceinline__ void scan_envs(const State<R>& S, const IO<R>& io, co
         const float lsp = __shfl(P.z, kc, kWave), lcp = __shfl(P.w, kc, kWave);
         const int lnl = (hb && !hasB) ? 0 : __shfl(nl, kc, kWave);
         Scan<float> sa, sb;
+        // (pass-1 marks: the tail of the other row buffer, past the <= 768 B the next DMA fills)
+        float* const oth = ((k / step) & 1) ? L.row0 : L.row1;
         lidar_wave2(cur, obst_stride(cap), lnl, lpx, lpy, ray_c(lcp, lsp, (float)kStartC, (float)kStartS),
-                    ray_s(lcp, lsp, (float)kStartC, (float)kStartS), L.rayoff, L.slot, L.mark, sa, sb);
+                    ray_s(lcp, lsp, (float)kStartC, (float)kStartS), L.rayoff, L.slot, L.mark,
+                    reinterpret_cast<int*>(oth) + 192, sa, sb);
         prof.mark(2);
         emit(k, sa);
         if (hasB) emit(k + 1, sb);
@@ -1910,7 +1960,7 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
       Scan<float> sa, sb;
       QMARK(1);
       lidar_wave2(cbuf, os, (hb && !hasB) ? 0 : (nt & 0xffff), pose.x, pose.y, pose.z, pose.w, rayoff, slot,
-                  mark, sa, sb, qp);
+                  mark, reinterpret_cast<int*>(nbuf) + 192, sa, sb, qp);
       float4 pose_n = pose, meta_n = meta;
       float hv_n = hv;
       if (nxt >= 0) rec_of(nxt, pose_n, meta_n, hv_n);   // the next pair's record (wave-uniform)
