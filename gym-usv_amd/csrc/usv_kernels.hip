@@ -1320,6 +1320,10 @@ template <typename R> __host__ __device__ constexpr size_t wave_tab_bytes() { re
 template <typename R> __host__ __device__ constexpr size_t scan_rowbuf_bytes(int cap) {
   return align16(std::max((size_t)2 * row_bytes<R>(cap), (size_t)64 * 4 * sizeof(R)));
 }
+// lidar_wave2 keeps pass-1 owner marks (64 ints) in the tail of the row buffer the next two-env DMA
+// fills (cap <= 32: two rows), in the wave-scan slices and in the block queue's 1 KiB row buffers
+static_assert(2 * row_bytes<float>(32) + 64 * 4 <= (int)scan_rowbuf_bytes<float>(32), "f32 mark2 tail");
+static_assert(2 * row_bytes<float>(32) + 64 * 4 <= 1024, "block-queue mark2 tail");
 template <typename R> __host__ __device__ constexpr size_t lds_scan_slice(int cap) {
   return 256 * 8 + 64 * 4 + 2 * scan_rowbuf_bytes<R>(cap);
 }
