@@ -2132,6 +2132,14 @@ constexpr int kFamV0 = 0, kFamYeInt = 1, kFamPid = 2;   // usv-asmc-v0, usv-asmc
 
 template <typename R> __device__ __forceinline__ R q32(R x) { return R((float)x); }
 
+// sin / cos of the legacy path angle ak.  The legacy resets put the target on the start's line
+// (yd = y0, usv_asmc_env.py:277-282), so ak = atan2(0, xd - x0) = +0 in every episode: a wave whose
+// lanes all hold ak = 0 takes sin 0 = 0, cos 0 = 1 (the values libm returns) without the two libm calls.
+template <typename R> __device__ __forceinline__ void v0_path_sincos(R ak, R& sa, R& ca) {
+  if (__builtin_amdgcn_ballot_w64(ak != R(0)) == 0) { sa = R(0); ca = R(1); }
+  else { sa = m_sin(ak); ca = m_cos(ak); }
+}
+
 template <typename R>
 __device__ __forceinline__ void v0_obs(float* row, R u, R v_ak, R r, R ye, R psi_ak, R a_last) {
   row[0] = (float)u; row[1] = (float)v_ak; row[2] = (float)r;
@@ -2297,7 +2305,9 @@ __global__ __launch_bounds__(kBlock) void v0_step_kernel(State<R> S, IO<R> io) {
   y = R(H) * (yd + yd_l) / R(2) + y;
   psi = wrap_once(R(H) * (pd + pd_l) / R(2) + psi);                              // :228-229
   const R psi_ak = wrap_once(psi - ak);                                          // :231-232
-  const R ye = -(x - x0) * m_sin(ak) + (y - y0) * m_cos(ak);                     // :234
+  R sak, cak;
+  v0_path_sincos(ak, sak, cak);
+  const R ye = -(x - x0) * sak + (y - y0) * cak;                                 // :234
   const R ye_abs = m_abs(ye);
   // compute_reward (:364-374)
   const R pa = m_abs(psi_ak);
@@ -2434,7 +2444,9 @@ __global__ __launch_bounds__(kBlock) void legacy_step_kernel(State<R> S, IO<R> i
   y = R(H) * (yd + yd_l) / R(2) + y;
   psi = wrap_once(R(H) * (pd + pd_l) / R(2) + psi);                              // :221-222
   const R psi_ak = wrap_once(psi - ak);                                          // :224-225
-  const R ye = -(x - x0) * m_sin(ak) + (y - y0) * m_cos(ak);                     // :227
+  R sak, cak;
+  v0_path_sincos(ak, sak, cak);
+  const R ye = -(x - x0) * sak + (y - y0) * cak;                                 // :227
   const R ye_abs = m_abs(ye);
   const R pa = m_abs(psi_ak);
   const R r_act = R(kV0WAction) * tanh(R(-kV0CAction) * (action_dot * action_dot));
