@@ -418,6 +418,65 @@ def test_step_variants_bit_identical_scattered(precision):
             assert torch.equal(x, y), f"variant {v} differs"
 
 
+def _window_pairs(e):
+    """Host estimate of the window lidar's (obstacle, ray) pairs per env at the current pose: the
+    rays (128 over 240 degrees from heading - 120, usv_asmc_ca_env.py:411-427) within asin(r / d) of
+    the obstacle's bearing, all 128 when the boat is inside it."""
+    res = np.deg2rad(240.0) / 128
+    dx, dy = e.ox - e.position[:, :1], e.oy - e.position[:, 1:2]
+    d = np.hypot(dx, dy)
+    half = np.arcsin(np.clip(e.orad / np.maximum(d, 1e-9), 0, 1))
+    ray = e.position[:, 2:3, None] - np.deg2rad(120.0) + res * np.arange(128)[None, None, :]
+    diff = np.angle(np.exp(1j * (ray - np.arctan2(dy, dx)[:, :, None])))
+    cnt = np.where(d <= e.orad, 128, (np.abs(diff) <= half[:, :, None]).sum(2))
+    valid = np.arange(e.ox.shape[1])[None, :] < e.n_obs[:, None]
+    return (cnt * valid).sum(1)
+
+
+@pytest.mark.parametrize("precision", ["f32", "f64"])
+def test_step_variants_bit_identical_crowded(precision):
+    """Variant bit-identity where the window lidar's pair list is long: the boat sits next to or
+    inside clusters of obstacles, so windows span up to all 128 rays and an env pair's list runs to
+    2-4 passes of 64 (the window kernels do passes 0 and 1 together and the rest one at a time);
+    brute-force variants are the reference."""
+    n = 2048
+    orc = O.OracleVectorEnv("usv-simple", n)
+    orc.reset(list(range(300, 300 + n)))
+    e = orc.env
+    rng = np.random.default_rng(23)
+    # pull obstacles 1..k around obstacle 0 and park the boat beside it (every 4th env inside it)
+    for i in range(n):
+        m = int(e.n_obs[i])
+        k = min(m - 1, int(rng.integers(2, 8)))
+        cx, cy = e.ox[i, 0], e.oy[i, 0]
+        ang = rng.uniform(0, 2 * np.pi, k)
+        dist = rng.uniform(0.5, 3.0, k)
+        e.ox[i, 1:1 + k] = cx + dist * np.cos(ang)
+        e.oy[i, 1:1 + k] = cy + dist * np.sin(ang)
+        off = 0.0 if i % 4 == 0 else rng.uniform(0.6, 2.5)
+        th = rng.uniform(0, 2 * np.pi)
+        e.position[i, 0] = np.clip(cx + off * np.cos(th), 0.05, 99.95)
+        e.position[i, 1] = np.clip(cy + off * np.sin(th), 0.05, 99.95)
+    e.position[:, 2] = rng.uniform(-np.pi, np.pi, n)
+    assert (_window_pairs(e).reshape(-1, 2).sum(1) > 128).mean() > 0.3   # >= 3 passes per env pair
+    a = torch.from_numpy(rng.uniform([0.2, -1], [1, 1], size=(n, 2)).astype(np.float32)).cuda()
+    ref = None
+    queue = ("128,7,4", "128,7,5", "16,7,5") if precision == "f32" else ("64,7,2", "64,7,3", "32,7,3")
+    for v in ("64,0,1", "32,3,1", "64,7,1", "16,7,2", "8,7,2") + queue:
+        env = make("usv-simple", n, seed=3, precision=precision, kernel_variant=v, copy=False)
+        inject(env, e, elapsed=1)
+        o, r, te, tr, info = env.step(a)
+        out = [x.clone() for x in (o, r, te, tr, info["final_obs"])]
+        env.close()
+        if ref is None:
+            ref = out
+            # the scenes are what they claim: many readings short of max range
+            assert float((out[0][:, 15:] < 0.05).float().mean()) > 0.2
+            continue
+        for x, y in zip(ref, out):
+            assert torch.equal(x, y), f"variant {v} differs"
+
+
 # --------------------------------------------------------------------------- usv-asmc-v0 (legacy)
 def _v0_inject(env, o, first):
     env.set_state({"x": o.position[:, 0], "y": o.position[:, 1], "psi": o.position[:, 2],
