@@ -975,8 +975,11 @@ __device__ __forceinline__ void lidar_window2(float dx, float dy, float key, flo
   // gives hr = 32.05), and a narrower window never wraps onto the rays.  ceil(v) = -floor(-v)
   // (v_cvt_flr_i32_f32: floor and convert in one instruction)
   const bool wide = hr >= 32.0f;
-  const int lo = wide ? 0 : max(0, -cvt_flr_i32(hr - pr));
-  const int hi = wide ? 127 : min(127, cvt_flr_i32(pr + hr));
+  // both converts unconditionally (the conversion saturates on a wide window's large operands): with a
+  // convert inside each select arm the compiler branches on exec around it, twice per env pair
+  const int flo = cvt_flr_i32(hr - pr), fhi = cvt_flr_i32(pr + hr);
+  const int lo = wide ? 0 : max(0, -flo);
+  const int hi = wide ? 127 : min(127, fhi);
   const int cnt = valid ? max(0, hi - lo + 1) : 0;
   const int incl = wave_incl_scan(cnt);
   const int off = wave_excl_of(incl);
