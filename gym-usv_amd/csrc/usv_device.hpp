@@ -390,10 +390,11 @@ __device__ __forceinline__ void asmc_substep(R (&s)[kAsmcN], R a0, R a1, R& x, R
 //    |v|, |r| and |nu| with the scale factors of :101-108 folded into its coefficients;
 //  * trapezoids H (a + b) / 2 + c as one fma by H / 2; ((r_d - o) F1 - F3 o') F2 with F = 2 as
 //    4 ((r_d - o) - o') (:86; bit-identical); np.sign products as copysign.
-//  * the pose (x, y, psi) integrates with compensated summation: xl, yl, pl carry what each substep's
-//    addition rounded away, and the caller folds them in after the 20 substeps, so a ~50 m float
-//    position is rounded once per env step instead of 20 times (the reward's ye term amplifies that
-//    rounding: golden replay reward error 1.0e-4 -> 3.5e-5 for +2 % of the dynamics kernel).
+//  * a ~50 m float position rounded at each of the 20 substeps was the f32 path's largest error (the
+//    reward's ye term amplifies it), so the position is rounded once per env step: x and y are not
+//    read inside the substep, so xl, yl accumulate their increments and the caller adds them after the
+//    20 substeps; psi is read by the next substep, so it integrates with compensated summation (pl
+//    carries what each addition rounded away; golden replay reward error 1.0e-4 -> 3.5e-5).
 __device__ __forceinline__ void asmc_substep_f32(float (&s)[kAsmcN], float a0, float a1, float& x, float& y,
                                                  float& psi, float& u, float& v, float& r, float& xl, float& yl,
                                                  float& pl, int pstep = 0, bool perturb = false) {
@@ -464,11 +465,11 @@ __device__ __forceinline__ void asmc_substep_f32(float (&s)[kAsmcN], float a0, f
   const float xd = fmaf(cp, u, -(sp * v)), yd = fmaf(sp, u, cp * v);          // :233
   {                                                                             // :234
     const float ix = (xd + s[4]) * h2, iy = (yd + s[5]) * h2, ip = (r + s[6]) * h2;
-    const float sx = x + ix, sy = y + iy, sq = psi + ip;
-    xl += ix - (sx - x);                                                        // fast two-sum errors
-    yl += iy - (sy - y);
-    pl += ip - (sq - psi);
-    x = sx; y = sy; psi = sq;
+    xl += ix;                                                                   // x, y: added by the caller
+    yl += iy;
+    const float sq = psi + ip;
+    pl += ip - (sq - psi);                                                      // fast two-sum error
+    psi = sq;
   }
   s[4] = xd; s[5] = yd; s[6] = r;
 }

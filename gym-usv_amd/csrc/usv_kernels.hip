@@ -541,7 +541,7 @@ __device__ void env_dynamics(const State<R>& S, int e, float a_u, float a_r, flo
     // perturb_step of the episode's UsvAsmc: 2 compute() x 10 substeps per env step (usv_asmc.py:199)
     const bool pert = S.perturb != 0;
     if constexpr (std::is_same<R, float>::value) {
-      float xl = 0.0f, yl = 0.0f, pl = 0.0f;        // compensation terms of the pose (asmc_substep_f32)
+      float xl = 0.0f, yl = 0.0f, pl = 0.0f;        // position increments, heading compensation (asmc_substep_f32)
       // perturbation hoisted out of the substep loop, so the common loop unrolls (by 4): no
       // loop-carried register rotation (the s[1..3], s[4..9] moves) and the scheduler fills one
       // substep's hazard nops with the next one's independent work (dyn_rec_kernel 13.6 -> 11.4 us
