@@ -397,7 +397,7 @@ __device__ __forceinline__ void asmc_substep(R (&s)[kAsmcN], R a0, R a1, R& x, R
 //    carries what each addition rounded away; golden replay reward error 1.0e-4 -> 3.5e-5).
 __device__ __forceinline__ void asmc_substep_f32(float (&s)[kAsmcN], float a0, float a1, float& x, float& y,
                                                  float& psi, float& u, float& v, float& r, float& xl, float& yl,
-                                                 float& pl, int pstep = 0, bool perturb = false) {
+                                                 float& pl, float kt, int pstep = 0, bool perturb = false) {
   constexpr float h2 = float(H / 2);
   const float au = fabsf(u), av = fabsf(v), ar = fabsf(r);
   const float vmag = __builtin_amdgcn_sqrtf(fmaf(u, u, v * v));
@@ -442,8 +442,11 @@ __device__ __forceinline__ void asmc_substep_f32(float (&s)[kAsmcN], float a0, f
   const float md12 = fmaf(float(YR_K), vmag, fmaf(float(YRV), av, float(YRR) * ar));
   const float md21 = fmaf(float(NV_K), vmag, fmaf(float(NVV), av, float(NVR) * ar));
   const float md22 = fmaf(float(NR_K), vmag, fmaf(float(NRV), av, float(NRR) * ar));
-  float sp, cp;
-  fx_sincos(psi, &sp, &cp);                                                     // J(psi_old) :179
+  // J(psi_old) (:179): psi reduced by the env step's whole turns kt (reduce_2pi's two-constant step with
+  // k fixed for the 20 substeps: psi moves well under a turn in one env step, so the reduced argument
+  // stays within about half a turn of zero, where v_sin / v_cos are accurate)
+  const float pr = fmaf(kt, 1.74845553e-07f, fmaf(-kt, 6.28318548f, psi));
+  const float sp = __sinf(pr), cp = __cosf(pr);
   float tt0 = tx, tt1 = 0.0f;
   if (perturb) {                                                                // T += F @ J (:184-198)
     double fx, fy;

@@ -542,15 +542,16 @@ __device__ void env_dynamics(const State<R>& S, int e, float a_u, float a_r, flo
     const bool pert = S.perturb != 0;
     if constexpr (std::is_same<R, float>::value) {
       float xl = 0.0f, yl = 0.0f, pl = 0.0f;        // position increments, heading compensation (asmc_substep_f32)
+      const float kt = rintf(psi * 0.159154943f);    // whole turns of the heading (asmc_substep_f32's J)
       // perturbation hoisted out of the substep loop, so the common loop unrolls (by 4): no
       // loop-carried register rotation (the s[1..3], s[4..9] moves) and the scheduler fills one
       // substep's hazard nops with the next one's independent work (dyn_rec_kernel 13.6 -> 11.4 us
       // at 65 536 envs)
       if (pert) {
-        for (int k = 0; k < 20; ++k) asmc_substep_f32(s, c0, c1, x, y, psi, u, v, r, xl, yl, pl, 20 * el0 + k, true);
+        for (int k = 0; k < 20; ++k) asmc_substep_f32(s, c0, c1, x, y, psi, u, v, r, xl, yl, pl, kt, 20 * el0 + k, true);
       } else {
 #pragma unroll 4
-        for (int k = 0; k < 20; ++k) asmc_substep_f32(s, c0, c1, x, y, psi, u, v, r, xl, yl, pl, 0, false);
+        for (int k = 0; k < 20; ++k) asmc_substep_f32(s, c0, c1, x, y, psi, u, v, r, xl, yl, pl, kt, 0, false);
       }
       x += xl; y += yl; psi += pl;
     } else {
