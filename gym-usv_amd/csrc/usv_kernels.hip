@@ -523,6 +523,42 @@ __global__ __launch_bounds__(kBlock) void exp_autoreset_kernel(State<R> S, IO<R>
   reset_experiment<R>(S, e, S.I(I_EPISODE)[e] - 1, io.obs + (size_t)e * kObsDim, nullptr);
 }
 
+// --------------------------------------------------------------------------- UsvAsmc.compute
+// The controller on its own (gym_usv/control/usv_asmc.py:53-244), lane per controller: `calls`
+// back-to-back compute() calls of 10 substeps each on [n][3] poses / velocities and the [16][n]
+// state (asmc_substep's layout).  Same substep functions as the env step; the f32 build applies
+// asmc_substep_f32's per-call pose accumulation (10 substeps here, 20 in an env step).
+template <typename R>
+__global__ __launch_bounds__(kBlock) void asmc_compute_kernel(int n, const R* __restrict__ act, R* pos, R* vel,
+                                                              R* st, int* pstep, int perturb, int calls) {
+  const int e = blockIdx.x * kBlock + threadIdx.x;
+  if (e >= n) return;
+  R s[kAsmcN];
+#pragma unroll
+  for (int i = 0; i < kAsmcN; ++i) s[i] = st[(size_t)i * n + e];
+  R x = pos[3 * (size_t)e], y = pos[3 * (size_t)e + 1], psi = pos[3 * (size_t)e + 2];
+  R u = vel[3 * (size_t)e], v = vel[3 * (size_t)e + 1], r = vel[3 * (size_t)e + 2];
+  const R a0 = act[2 * (size_t)e], a1 = act[2 * (size_t)e + 1];
+  int ps = pstep ? pstep[e] : 0;
+  const bool pert = perturb != 0;
+  for (int c = 0; c < calls; ++c) {
+    if constexpr (std::is_same<R, float>::value) {
+      float xl = 0.0f, yl = 0.0f, pl = 0.0f;
+      const float kt = rintf(psi * 0.159154943f);
+      for (int k = 0; k < 10; ++k) asmc_substep_f32(s, a0, a1, x, y, psi, u, v, r, xl, yl, pl, kt, ps + k, pert);
+      x += xl; y += yl; psi += pl;
+    } else {
+      for (int k = 0; k < 10; ++k) asmc_substep<R>(s, a0, a1, x, y, psi, u, v, r, ps + k, pert);
+    }
+    ps += 10;                                                   // perturb_step (:199)
+  }
+#pragma unroll
+  for (int i = 0; i < kAsmcN; ++i) st[(size_t)i * n + e] = s[i];
+  pos[3 * (size_t)e] = x; pos[3 * (size_t)e + 1] = y; pos[3 * (size_t)e + 2] = psi;
+  vel[3 * (size_t)e] = u; vel[3 * (size_t)e + 1] = v; vel[3 * (size_t)e + 2] = r;
+  if (pstep) pstep[e] = ps;
+}
+
 // --------------------------------------------------------------------------- phase 1
 // UsvSimpleEnv.step kinematics..reward terms (simple_env.py:310-346); for usv-asmc-simple
 // first 2x UsvAsmc.compute (simple_env_asmc.py:18-27) and then step(zeros(2)).
@@ -1430,9 +1466,9 @@ __device__ __forceinline__ void emit_env(const State<R>& S, const IO<R>& io, int
       float* f = io.fobs + (size_t)e * kObsDim;
       f[kHdr + l] = s0;
       f[kHdr + 64 + l] = s1;
-      // header: written earlier by this wave (wave kernel) or by dyn_kernel; a wavefront's
-      // own earlier stores are visible to its later loads
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // header: written earlier by this wave (wave kernel), by dyn_kernel, or by wave 0 of this
+      // block (kind 3, released before the block barrier)
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
       if (l < kHdr) f[l] = row[l];
     }
     if (S.autoreset == USV_AUTORESET_SAME_STEP) {
@@ -1719,8 +1755,14 @@ __device__ __forceinline__ void step_body_blockdyn(const State<R>& S, const IO<R
     rec[l] = R4<R>{px, py, sp, cp};
     rec[kWave + l] = R4<R>{partial, R(S.I(I_NOBS)[e]), R(trunc ? 1 : 0), R(0)};
     USV_STAMP_W(1);
-    // the prologue DMA landed: the header stores above were issued after it
-    vm_wait<2>();
+    if (io.fobs) {
+      // waves 1-3 read these header rows back for their done envs' terminal obs (emit_env): every
+      // header store complete and released to the workgroup before the barrier
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      vm_wait<0>();
+    } else {
+      vm_wait<2>();   // the prologue DMA landed: the header stores above were issued after it
+    }
   } else {
     vm_wait<0>();
   }
@@ -2974,6 +3016,26 @@ int usv_diag_stamps(void* host, size_t bytes) {
 
 const char* usv_last_error(void) { return g_err.c_str(); }
 
+size_t usv_config_size(void) { return sizeof(usv_config); }
+
+int usv_asmc_compute(int32_t precision, int32_t n, const void* act, void* pos, void* vel, void* state,
+                     int32_t* perturb_step, int32_t do_perturb, int32_t calls, void* stream) {
+  if (precision != USV_F32 && precision != USV_F64) return fail(USV_ERR_ARG, "unknown precision");
+  if (n < 0 || calls < 0) return fail(USV_ERR_ARG, "n and calls must be >= 0");
+  if (n == 0 || calls == 0) return USV_OK;
+  if (!act || !pos || !vel || !state) return fail(USV_ERR_ARG, "null argument");
+  const dim3 grid((n + kBlock - 1) / kBlock), block(kBlock);
+  hipStream_t st = (hipStream_t)stream;
+  if (precision == USV_F32)
+    hipLaunchKernelGGL(asmc_compute_kernel<float>, grid, block, 0, st, n, (const float*)act, (float*)pos,
+                       (float*)vel, (float*)state, perturb_step, do_perturb, calls);
+  else
+    hipLaunchKernelGGL(asmc_compute_kernel<double>, grid, block, 0, st, n, (const double*)act, (double*)pos,
+                       (double*)vel, (double*)state, perturb_step, do_perturb, calls);
+  HIP_TRY(hipGetLastError());
+  return USV_OK;
+}
+
 void usv_config_default(usv_config* cfg, int32_t mode, int32_t num_envs) {
   if (!cfg) return;
   std::memset(cfg, 0, sizeof(*cfg));
@@ -3066,11 +3128,15 @@ int usv_set_kernel_variant(void* hp, int32_t kind, int32_t epb, int32_t lid) {
   if (!(wave_ok || split_ok || blockdyn_ok || queue_ok)) return fail(USV_ERR_ARG, "kernel variant not available for this config");
   DeviceGuard g(h->device);
   HIP_TRY(hipDeviceSynchronize());                 // launches in flight keep the variant they took
+  Handle trial = *h;                               // raise the new variant's LDS limit first, and
+  trial.kind = kind;                               // commit it to the handle only if that worked
+  trial.epb = epb;
+  if (const int rc = queue_lds_attr(&trial); rc != USV_OK) return rc;
   h->kind = kind;
   h->epb = epb;
   h->lid = lid;
   h->prio = (kind == 4 || kind == 5) ? 0 : 1;
-  return queue_lds_attr(h);
+  return USV_OK;
 }
 
 void usv_destroy(void* hp) {

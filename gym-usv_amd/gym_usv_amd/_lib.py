@@ -14,7 +14,7 @@ LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), LIB_NAME)
 # diagnostic builds (tools/) may point at another in-tree copy of the library
 LIB_PATH = os.environ.get("USV_LIB_PATH", LIB_PATH)
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 MODE_SIMPLE, MODE_ASMC_SIMPLE, MODE_ASMC_V0, MODE_ASMC_YE_INT_V0, MODE_PID_V0 = 0, 1, 2, 3, 4
 F32, F64 = 0, 1
 AUTORESET_SAME_STEP, AUTORESET_DISABLED = 0, 1
@@ -82,6 +82,8 @@ SIGNATURES = [
     ("usv_get_state", ctypes.c_int, [_vp, _vp, _sz]),
     ("usv_set_state", ctypes.c_int, [_vp, _vp, _sz]),
     ("usv_set_kernel_variant", ctypes.c_int, [_vp, _i32, _i32, _i32]),
+    ("usv_config_size", _sz, []),
+    ("usv_asmc_compute", ctypes.c_int, [_i32, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _i32, _vp]),
 ]
 
 _LIBS = {}
@@ -106,6 +108,9 @@ def load(path=None):
         fn.argtypes = args
     if lib.usv_abi_version() != ABI_VERSION:
         raise UsvLibError("libusvhip ABI version mismatch")
+    if lib.usv_config_size() != ctypes.sizeof(UsvConfig):
+        raise UsvLibError(f"usv_config is {lib.usv_config_size()} B in the library, "
+                          f"{ctypes.sizeof(UsvConfig)} B in this binding")
     _LIBS[path] = lib
     return lib
 

@@ -16,7 +16,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
-from .vector_env import UsvVectorEnv
+from .vector_env import LEGACY_IDS, UsvVectorEnv
 
 
 class _SingleEnv:
@@ -40,7 +40,10 @@ class _SingleEnv:
 
     def reset(self, seed=None, options=None):
         if seed is None and not self._seeded:
-            seed = int(np.random.SeedSequence().entropy % (1 << 63))
+            # an unseeded first reset draws fresh entropy (gymnasium's np_random(None)); the legacy ids
+            # seed np.random's MT19937, which takes seeds below 2**32 only (usv_asmc_env.py:258)
+            bound = 1 << (32 if self.env_id in LEGACY_IDS else 63)
+            seed = int(np.random.SeedSequence().entropy % bound)
         if seed is not None:
             self._seeded = True
         obs, info = self._venv.reset(seed=seed, options=options)

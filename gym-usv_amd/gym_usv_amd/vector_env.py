@@ -247,11 +247,14 @@ class UsvVectorEnv:
         m = None
         if mask is not None:
             m = torch.as_tensor(mask, device=self.device).to(torch.uint8).contiguous()
-        # rows of envs that are not reset keep the latest obs (and info) rows
-        obs = self._last_obs.clone() if self.copy else self._last_obs
-        ib = self.info_buf
-        if self.info_enabled and self.copy:
-            ib = self.info_buf.clone()
+        # rows of envs that are not reset keep the latest obs (and info) rows; a full reset rewrites
+        # every row, so with copy=True it only needs fresh tensors
+        obs, ib = self._last_obs, self.info_buf
+        if self.copy:
+            fresh = torch.empty_like if m is None else torch.clone
+            obs = fresh(obs)
+            if self.info_enabled:
+                ib = fresh(ib)
         self._check(self.lib.usv_reset_ex(self._h, _ptr(m), _ptr(obs), ctypes.byref(ropt),
                                          _ptr(ib), _stream_ptr(self.device)))
         self._last_obs = obs

@@ -27,6 +27,8 @@
  *                      legacy UsvAsmcEnv.step (usv_asmc_env.py:99-255, compute_reward :364-374),
  *                      UsvAsmcYeIntEnv.step (usv_asmc_ye_int_env.py:92-253, :350-360),
  *                      UsvPidEnv.step (usv_pid_env.py:89-233, :329-338)
+ *   usv_asmc_compute <- UsvAsmc.compute (gym_usv/control/usv_asmc.py:53-244), the controller
+ *                      on its own, as the reference's tests drive it (tests/test_usv_asmc.py:8-37)
  *   usv_get_field / usv_set_field / usv_get_state / usv_set_state
  *                   <- the env attributes (position, velocity, obstacle_positions, ...);
  *                      used for checkpointing and for parity state injection
@@ -48,7 +50,7 @@
 extern "C" {
 #endif
 
-#define USV_ABI_VERSION 4
+#define USV_ABI_VERSION 5
 #define USV_SENSOR_COUNT 128
 #define USV_OBS_DIM 143      /* 15 + 128, simple_env.py:27 */
 #define USV_ACT_DIM 2        /* simple_env.py:30 */
@@ -188,6 +190,9 @@ typedef enum usv_field {
 
 int usv_abi_version(void);
 const char* usv_last_error(void);
+/* sizeof(usv_config) as compiled into the library (56): a binding checks its own struct against it
+ * (ABI v5). */
+size_t usv_config_size(void);
 
 /* Fill `cfg` with the reference defaults for `mode` (cap 32, TimeLimit by id -- 500, 1000,
  * none for the legacy *-v0 ids --, f32, same-step autoreset, window lidar, seed 0). */
@@ -239,6 +244,20 @@ int usv_step(void* handle, const float* act_dev, float* obs_dev, void* rew_dev,
 int usv_step_ex(void* handle, const float* act_dev, float* obs_dev, void* rew_dev,
                 uint8_t* term_dev, uint8_t* trunc_dev, uint8_t* done_dev, float* final_obs_dev,
                 void* info_dev, void* stream);
+
+/* UsvAsmc.compute(action, position, velocity, do_perturb) (gym_usv/control/usv_asmc.py:53-244) for
+ * n independent controllers, `calls` compute() calls back to back (10 substeps of 0.01 s each), in
+ * place on device buffers of the precision's type (float for USV_F32, double for USV_F64):
+ *   act_dev [n][2] (u_d, heading offset), pos_dev [n][3] (x, y, psi), vel_dev [n][3] (u, v, r),
+ *   state_dev [16][n]: psi_d_last, o, o', o'', eta_dot_last[3], upsilon_dot_last[3], e_u_last,
+ *     Ka_dot_u_last, Ka_dot_psi_last, e_u_int, Ka_u, Ka_psi (so_filter / last / aux_vars, :43-49;
+ *     the reference keeps so_filter's o_last, o_dot_last, o_dot_dot_last equal to o, o', o'');
+ *   perturb_step_dev int32 [n] or NULL (= 0): the controllers' perturb_step (:49), advanced by 10
+ *     per call; do_perturb adds the sinusoidal disturbance (:184-199).
+ * Stream-ordered, no handle (ABI v5). */
+int usv_asmc_compute(int32_t precision, int32_t n, const void* act_dev, void* pos_dev, void* vel_dev,
+                     void* state_dev, int32_t* perturb_step_dev, int32_t do_perturb, int32_t calls,
+                     void* stream);
 
 /* Select the step-kernel variant of a usv-simple / usv-asmc-simple handle (verification and
  * tuning: every variant computes bit-identical outputs, tests/test_gpu_*.py compare them bitwise).

@@ -123,6 +123,7 @@ class AsmcBatch:
     def __init__(self, n):
         self.state = np.zeros((n, ASMC_N))
         self.perturb_step = np.zeros(n, dtype=np.int64)                   # usv_asmc.py:49
+        self.fast_substeps = np.zeros(n, dtype=np.int64)   # checker statistic: substeps with |u| > 1.2
 
     def reset(self, idx=None):
         if idx is None:
@@ -152,6 +153,7 @@ class AsmcBatch:
             o_d, o_dd = o_d_new, o_dd_new
             r_d = o                                                       # :89
             fast = np.abs(u) > 1.2                                        # :95-99
+            self.fast_substeps += fast
             xu = np.where(fast, 64.55, -25.0)
             xuu = np.where(fast, -70.92, 0.0)
             vmag = np.sqrt(u * u + v * v)

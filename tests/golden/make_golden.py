@@ -18,6 +18,9 @@ reference source travels.  Fixtures:
                             (usv-asmc-ye-int-v0) and UsvPidEnv (usv-pid-v0), same protocol
                             (``python tests/golden/make_golden.py --legacy-f64`` makes only these).
 
+Round 4 (``--r4``): ``asmc_highspeed.npz`` -- usv-asmc-simple steps from injected high-speed /
+large-heading / large-gain states, with and without do_perturb (gen_asmc_highspeed).
+
 Round 2 (``--r2`` makes only these):
 
 * ``asmc_perturb_traj.npz`` -- usv-asmc-simple rollouts with UsvAsmc.compute(..., do_perturb=True)
@@ -434,9 +437,94 @@ def gen_path_rollouts(E, fname="path_traj.npz", per_k=6, T=100):
     print(fname, "n_obs", st["init_n_obs"], "steps", steps)
 
 
+# --------------------------------------------------------------------------- round-4 fixtures
+def _f32(x):
+    """Round to the nearest float32 (kept as float64): injected states every precision holds exactly."""
+    return np.asarray(x, dtype=np.float32).astype(np.float64)
+
+
+def gen_asmc_highspeed(E, fname="asmc_highspeed.npz", n_env=48, T=8):
+    """usv-asmc-simple steps (simple_env_asmc.py:18-27) from harness-injected states outside the
+    low-speed regime the action space reaches: u in [-1, 4] (UsvAsmc's |u| > 1.2 hydrodynamics,
+    usv_asmc.py:95-99), r in [-1, 1], v in [-0.1, 0.1] (the reference's explicit integrator diverges
+    for |v| above ~0.3: Yv's damping, ~19 880 |v| over m - Y_v_dot = 53.13 (:101-102, :172-174), puts
+    h * lambda past its stability bound), headings up to +-400 rad, adaptive gains up to 5, filter and
+    integral states far from zero, desired speeds u_d up to 10 (the reference KATs'
+    tests/test_usv_asmc.py:18-37).  Odd envs run UsvAsmc.compute(..., do_perturb=True)
+    (usv_asmc.py:184-199) with perturb_step = 20 * elapsed.  Every injected value is a float32, so the
+    f32 kernel starts from the state the reference starts from.  Recorded per step up to each env's
+    first episode end: obs, reward, flags, the info position / velocity and the ASMC state."""
+    from gym_usv.control.usv_asmc import UsvAsmc
+
+    class PerturbedASMCEnv(E.UsvSimpleASMCEnv):
+        def step(self, action):
+            for _ in range(2):
+                self.position, self.velocity, _ = self.asmc.compute(action, self.position, self.velocity, True)
+            return E.UsvSimpleEnv.step(self, np.zeros(2))
+
+    rng = np.random.default_rng(4040)
+    perturb = (np.arange(n_env) % 2) == 1
+    seeds = np.arange(n_env) + 8000
+    acts = np.zeros((n_env, T, 2), np.float32)
+    acts[:, :, 0] = np.where(rng.uniform(size=(n_env, T)) < 0.6, rng.uniform(0.2, 10, (n_env, T)),
+                             rng.uniform(0.2, 1, (n_env, T)))
+    acts[:, :, 1] = rng.uniform(-1, 1, (n_env, T))
+    out = {k: [] for k in ("position", "velocity", "last_action", "so_in", "last_in", "aux_in", "elapsed")}
+    rec = {"final_obs": np.zeros((n_env, T, 143), np.float32), "reward": np.zeros((n_env, T)),
+           "terminated": np.zeros((n_env, T), bool), "truncated": np.zeros((n_env, T), bool),
+           "info_position": np.zeros((n_env, T, 3)), "info_velocity": np.zeros((n_env, T, 3)),
+           "so_out": np.zeros((n_env, T, 7)), "last_out": np.zeros((n_env, T, 9)),
+           "aux_out": np.zeros((n_env, T, 3)), "steps": np.zeros(n_env, np.int64)}
+    snaps = []
+    for e in range(n_env):
+        env = (PerturbedASMCEnv if perturb[e] else E.UsvSimpleASMCEnv)(render_mode=None)
+        env.reset(seed=int(seeds[e]))
+        band = e % 3                                  # heading scale: a turn, 30 rad, 400 rad
+        psi = rng.uniform(-np.pi, np.pi) if band == 0 else rng.uniform(-30, 30) if band == 1 else \
+            rng.choice([-1, 1]) * rng.uniform(300, 400)
+        pos = _f32([rng.uniform(4, 16), rng.uniform(4, 16), psi])
+        vel = _f32([rng.uniform(-1, 4), rng.uniform(-0.1, 0.1), rng.uniform(-1, 1)])
+        mx = env.max_action
+        la = _f32([rng.uniform(0, 0.5) * mx[0], 0.0, rng.uniform(-0.5, 0.5) * mx[2]])
+        pdl, o, od, odd = _f32([psi + rng.uniform(-0.5, 0.5), rng.uniform(-2, 2), rng.uniform(-20, 20),
+                                rng.uniform(-200, 200)])
+        so = np.array([pdl, odd, od, o, o, od, odd])
+        last = _f32(np.concatenate([rng.uniform(-4, 4, 3), rng.uniform(-5, 5, 3), [rng.uniform(-5, 5)],
+                                    [rng.choice([-0.1, 0.1, 0.05])], [rng.choice([-0.2, 0.2])]]))
+        aux = _f32([rng.uniform(-20, 20), rng.choice([0.02, rng.uniform(0, 5)]), rng.choice([0.1, rng.uniform(0, 5)])])
+        elapsed = int(rng.integers(0, 990))
+        env.position, env.velocity, env.last_action = pos.copy(), vel.copy(), la.copy()
+        env.asmc.so_filter, env.asmc.last, env.asmc.aux_vars = so.copy(), last.copy(), aux.copy()
+        env.asmc.perturb_step = 20 * elapsed
+        for k, v in (("position", pos), ("velocity", vel), ("last_action", la), ("so_in", so), ("last_in", last),
+                     ("aux_in", aux), ("elapsed", elapsed)):
+            out[k].append(v)
+        snaps.append(snapshot(env))
+        for t in range(T):
+            o_, r, te, tr, inf = env.step(acts[e, t])
+            tr = bool(tr) or elapsed + t + 1 >= 1000
+            rec["final_obs"][e, t], rec["reward"][e, t] = o_, r
+            rec["terminated"][e, t], rec["truncated"][e, t] = bool(te), tr
+            rec["info_position"][e, t], rec["info_velocity"][e, t] = inf["position"], inf["velocity"]
+            rec["so_out"][e, t], rec["last_out"][e, t] = env.asmc.so_filter, env.asmc.last
+            rec["aux_out"][e, t] = env.asmc.aux_vars
+            rec["steps"][e] = t + 1
+            if te or tr:
+                break
+    st = {f"init_{k}": np.stack([np.asarray(s[k]) for s in snaps]) for k in snaps[0]
+          if k not in ("position", "velocity", "last_action")}
+    np.savez_compressed(os.path.join(HERE, fname), seeds=seeds, actions=acts, perturb=perturb,
+                        **{f"inj_{k}": np.stack([np.asarray(v) for v in vs]) for k, vs in out.items()}, **rec, **st)
+    print(fname, "steps", rec["steps"], "max |u| after a step", np.abs(rec["info_velocity"][..., 0]).max())
+    del UsvAsmc
+
+
 def main():
     refharness.load_reference()
     import gym_usv.envs as E
+    if "--r4" in sys.argv:              # round-4 fixtures only (existing files untouched)
+        gen_asmc_highspeed(E)
+        return
     if "--r3" in sys.argv:              # round-3 fixtures only (existing files untouched)
         gen_path_rollouts(E)
         gen_info_traj(E, fname="asmc_info_traj.npz", cls=E.UsvSimpleASMCEnv, seed0=5100)

@@ -1,0 +1,215 @@
+"""Round-4 GPU parity: the HIP ASMC outside the low-speed regime, and the controller on its own.
+
+* ``asmc_highspeed.npz`` (make_golden.py gen_asmc_highspeed): the reference's UsvSimpleASMCEnv
+  stepped from injected states with |u| up to 4 (the |u| > 1.2 hydrodynamics, usv_asmc.py:95-99),
+  headings to 400 rad, adaptive gains to 5 and u_d to 10, with and without do_perturb
+  (:184-199), replayed through the env's usv_set_state / usv_step.
+* ``gym_usv_amd.control.UsvAsmc`` (usv_asmc_compute): the reference's three tests
+  (tests/test_usv_asmc.py:8-37, adapted to compute(a, p, v, False) as SURVEY §4 states) and the
+  192 injected states and perturbed sequences of asmc_compute.npz / asmc_perturb_traj.npz.
+
+Tolerances: f64 to the reference's float64 arithmetic (the oracle matches the reference to 1e-9 on
+these fixtures); f32 per SURVEY §8(c) on obs / reward (obs 1e-5 + 1e-4 |ref|, reward 1e-4), the
+ASMC state relative to max(1, |ref|), each bound ~5x the measured error printed by the test.
+"""
+import numpy as np
+import pytest
+import torch
+
+from asmc_fixture import asmc_state, env_state, oracle_env
+
+pytestmark = pytest.mark.gpu
+
+
+def make(env_id, n, **kw):
+    import gym_usv_amd
+    return gym_usv_amd.make_vec(env_id, n, device=0, **kw)
+
+
+def to_np(*ts):
+    torch.cuda.synchronize()
+    return [t.detach().cpu().numpy() for t in ts]
+
+
+# f32 bounds, ~5x the measured worst case (printed); f64 bounds: the reference's arithmetic
+HS_TOL = {"f64": dict(hdr=2e-6, rew=1e-8, vel=1e-9, state=1e-9),
+          "f32": dict(hdr=1e-5, rew=1e-4, vel=5e-4, state=5e-3)}
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+@pytest.mark.parametrize("perturb", [False, True], ids=["plain", "perturb"])
+def test_asmc_highspeed_replay(golden, precision, perturb):
+    g = golden("asmc_highspeed.npz")
+    idx = np.flatnonzero(g["perturb"] == perturb)
+    n, T = len(idx), g["actions"].shape[1]
+    env = make("usv-asmc-simple", n, precision=precision, autoreset=False, info=True, perturb=perturb)
+    env.set_state(env_state(g, idx))
+    orc = oracle_env(g, idx, perturb)           # the checker: counts the |u| > 1.2 substeps
+    alive = np.ones(n, bool)
+    worst = dict(hdr=0.0, rew=0.0, vel=0.0, pos=0.0, state=0.0)
+    flips = rays = 0
+    orc_state = []
+    for t in range(T):
+        a = torch.from_numpy(g["actions"][idx, t]).cuda()
+        obs, rew, term, trunc, info = env.step(a)
+        obs, rew, term, trunc, ipos, ivel = to_np(obs, rew, term, trunc, info["position"], info["velocity"])
+        orc.step(g["actions"][idx, t])
+        orc_state.append(orc.asmc.state.copy())
+        m = alive
+        if not m.any():
+            break
+        ref = g["final_obs"][idx][m, t]
+        worst["hdr"] = max(worst["hdr"], float((np.abs(obs[m, :15] - ref[:, :15]) - 1e-4 * np.abs(ref[:, :15])).max()))
+        flips += int((np.abs(obs[m, 15:] - ref[:, 15:]) > 1e-5 + 1e-4 * np.abs(ref[:, 15:])).sum())
+        rays += int(m.sum()) * 128
+        worst["rew"] = max(worst["rew"], float(np.abs(rew[m] - g["reward"][idx][m, t]).max()))
+        rv = g["info_velocity"][idx][m, t]
+        worst["vel"] = max(worst["vel"], float((np.abs(ivel[m] - rv) / np.maximum(1, np.abs(rv))).max()))
+        rp = g["info_position"][idx][m, t]
+        worst["pos"] = max(worst["pos"], float((np.abs(ipos[m] - rp) / np.maximum(1, np.abs(rp))).max()))
+        st = env.get_field("asmc")
+        rs = asmc_state(g["so_out"][idx][m, t], g["last_out"][idx][m, t], g["aux_out"][idx][m, t])
+        worst["state"] = max(worst["state"], float((np.abs(st[m] - rs) / np.maximum(1, np.abs(rs))).max()))
+        np.testing.assert_array_equal(term[m], g["terminated"][idx][m, t], err_msg=f"t={t}")
+        np.testing.assert_array_equal(trunc[m], g["truncated"][idx][m, t], err_msg=f"t={t}")
+        alive &= ~(g["terminated"][idx][:, t] | g["truncated"][idx][:, t])
+    fast = int(orc.asmc.fast_substeps.sum())
+    print(f"\n[asmc highspeed {precision} perturb={perturb}] {fast} substeps with |u| > 1.2 over {n} envs; "
+          + ", ".join(f"{k} {v:.2e}" for k, v in worst.items()) + f"; sensor flips {flips}/{rays}")
+    assert fast > 0 and (orc.asmc.fast_substeps > 0).sum() >= n // 3
+    tol = HS_TOL[precision]
+    assert worst["hdr"] <= tol["hdr"] and worst["rew"] <= tol["rew"], worst
+    assert worst["vel"] <= tol["vel"] and worst["pos"] <= tol["vel"] and worst["state"] <= tol["state"], worst
+    assert flips <= (0 if precision == "f64" else max(2, rays // 10000))
+    env.close()
+
+
+# --------------------------------------------------------------------------- the controller on its own
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_reference_asmc_tests_on_hip(golden, precision):
+    """The reference's own tests (tests/test_usv_asmc.py:8-37: 1000 compute() calls from rest),
+    adapted to the signature the reference code has (compute(a, p, v, False), three return values;
+    SURVEY §4), run on the HIP controller.  f64 additionally follows the reference's trajectories
+    (the first 300 calls, before chaotic sign() switches amplify last-bit differences)."""
+    from gym_usv_amd.control import UsvAsmc
+    g = golden("asmc_compute.npz")
+    worst = 0.0
+    for name, act in (("kat_zero", [0, 0]), ("kat_fwd", [10, 0]), ("kat_rot", [0, 10])):
+        asmc = UsvAsmc(precision=precision)
+        position, velocity = np.zeros(3), np.zeros(3)
+        traj = []
+        for k in range(1000):
+            position, velocity, _ = asmc.compute(np.array(act, dtype=np.float64), position, velocity, False)
+            if k < 50 or k % 50 == 49:
+                traj.append(np.concatenate([position, velocity]))
+        traj = np.stack(traj)
+        if name == "kat_zero":                                       # test_no_movement :8-16
+            assert np.allclose(position, np.zeros(3)) and np.allclose(velocity, np.zeros(3))
+        elif name == "kat_fwd":                                      # test_forward_movement :18-28
+            assert position[0] > 10 and np.all(np.abs(position[1:]) < 1)
+            assert velocity[0] > 1 and np.all(np.abs(velocity[1:]) < 1)
+        else:                                                        # test_rotation :30-37
+            assert position[2] > 5
+        ref = g[name]
+        err = np.abs(traj[:55] - ref[:55]) / np.maximum(1, np.abs(ref[:55]))
+        worst = max(worst, float(err.max()))
+        print(f"\n[KAT {name} {precision}] final pos {position}, vel {velocity}; ref final {ref[-1]}; "
+              f"first 300 calls max rel err {err.max():.2e}")
+    assert worst <= (1e-9 if precision == "f64" else 5e-4), worst
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_asmc_compute_injected_states(golden, precision):
+    """UsvAsmc.compute on the 192 injected states of asmc_compute.npz (both Xu regimes, Ka switches),
+    one batched launch (UsvAsmcBatch)."""
+    from gym_usv_amd.control import UsvAsmcBatch
+    g = golden("asmc_compute.npz")
+    n = g["action"].shape[0]
+    b = UsvAsmcBatch(n, precision=precision)
+    b.state.copy_(torch.from_numpy(asmc_state(g["so_in"], g["last_in"], g["aux_in"]).T.copy()))
+    p, v = b.compute(g["action"], g["pos_in"], g["vel_in"])
+    p, v, st = to_np(p, v, b.state)
+    ref_st = asmc_state(g["so_out"], g["last_out"], g["aux_out"])
+    rel = lambda a, r: float((np.abs(a - r) / np.maximum(1, np.abs(r))).max())
+    e = dict(pos=rel(p, g["pos_out"]), vel=rel(v, g["vel_out"]), state=rel(st.T, ref_st))
+    print(f"\n[asmc compute 192 {precision}] " + ", ".join(f"{k} {x:.2e}" for k, x in e.items())
+          + f"; |u| > 1.2 inputs: {int((np.abs(g['vel_in'][:, 0]) > 1.2).sum())}")
+    tol = 1e-10 if precision == "f64" else dict(pos=2e-6, vel=5e-5, state=5e-4)
+    for k, x in e.items():
+        assert x <= (tol if precision == "f64" else tol[k]), (k, x)
+
+
+@pytest.mark.parametrize("precision", ["f64", "f32"])
+def test_asmc_compute_perturbed_sequences(golden, precision):
+    """UsvAsmc.compute(..., do_perturb=True) from fresh controllers, 120 calls (perturb_step 0 ..
+    1190; usv_asmc.py:184-199): the reference's sequences of asmc_perturb_traj.npz."""
+    from gym_usv_amd.control import UsvAsmcBatch
+    g = golden("asmc_perturb_traj.npz")
+    seq, act = g["compute_seq"], g["compute_act"]
+    b = UsvAsmcBatch(seq.shape[0], precision=precision)
+    pos = torch.from_numpy(seq[:, 0, :3].copy()).cuda().to(b.dtype)
+    vel = torch.from_numpy(seq[:, 0, 3:].copy()).cuda().to(b.dtype)
+    worst = 0.0
+    for k in range(1, 41):
+        b.compute(act, pos, vel, do_perturb=True)
+        got = np.concatenate(to_np(pos, vel), axis=1)
+        worst = max(worst, float((np.abs(got - seq[:, k]) / np.maximum(1, np.abs(seq[:, k]))).max()))
+    (ps,) = to_np(b.perturb_step)
+    print(f"\n[asmc perturb seq {precision}] 40 calls, max rel err {worst:.2e}")
+    assert np.all(ps == 400)
+    assert worst <= (1e-9 if precision == "f64" else 5e-4), worst
+
+
+def test_asmc_compute_matches_env_step_f64():
+    """The standalone controller and the env step run the same substep function: two compute()
+    calls from an env's state give the env step's ASMC state bit for bit (f64)."""
+    from gym_usv_amd.control import UsvAsmcBatch
+    n = 256
+    env = make("usv-asmc-simple", n, precision="f64", seed=3, autoreset=False)
+    env.reset(seed=3)
+    gen = torch.Generator(device="cuda").manual_seed(2)
+    for _ in range(5):
+        env.step(torch.rand(n, 2, device="cuda", generator=gen) * torch.tensor([0.8, 2.0], device="cuda")
+                 + torch.tensor([0.2, -1.0], device="cuda"))
+    st = env.get_state()
+    a = torch.rand(n, 2, device="cuda", generator=gen) * torch.tensor([0.8, 2.0], device="cuda") \
+        + torch.tensor([0.2, -1.0], device="cuda")
+    b = UsvAsmcBatch(n, precision="f64")
+    b.state.copy_(torch.from_numpy(st["asmc"].T.copy()))
+    pos = torch.from_numpy(np.stack([st["x"], st["y"], st["psi"]], 1)).cuda()
+    vel = torch.from_numpy(np.stack([st["u"], st["v"], st["r"]], 1)).cuda()
+    b.compute(a.double(), pos, vel, calls=2)
+    env.step(a)
+    (bst,) = to_np(b.state)
+    np.testing.assert_array_equal(bst.T, env.get_field("asmc"))
+    env.close()
+
+
+def test_integration_snippet_runs_verbatim_on_gpu():
+    """INTEGRATION.md §2's reference-side binding, executed as written (a fresh process with
+    libusvhip.so on LD_LIBRARY_PATH): create, reset, step, step_ex with info and done outputs."""
+    import os
+    import subprocess
+    import sys
+    from test_abi import integration_snippet
+    from gym_usv_amd import _lib
+    prog = integration_snippet() + ("torch.cuda.synchronize()\n"
+                                    "assert torch.isfinite(obs).all() and torch.isfinite(rew).all()\n"
+                                    "assert bool(((term | trunc) == done).all())\n"
+                                    "lib.usv_destroy.argtypes = [ctypes.c_void_p]\nlib.usv_destroy(h)\nprint('SNIPPET OK')\n")
+    env = dict(os.environ, LD_LIBRARY_PATH=os.path.dirname(_lib.LIB_PATH))
+    out = subprocess.run([sys.executable, "-c", prog], env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0 and "SNIPPET OK" in out.stdout, out.stderr[-2000:]
+
+
+@pytest.mark.parametrize("env_id", ["usv-asmc-v0", "usv-pid-v0", "usv-asmc-ye-int-v0", "usv-simple"])
+def test_unseeded_single_env_reset(env_id):
+    """gym_usv_amd.make(id).reset() with no seed, the reference's usual first call: the legacy ids
+    seed np.random's MT19937 (seeds below 2**32, usv_asmc_env.py:258) from fresh entropy."""
+    import gym_usv_amd
+    for _ in range(4):
+        env = gym_usv_amd.make(env_id)
+        out = env.reset()
+        obs = out if env_id != "usv-simple" else out[0]
+        assert np.isfinite(obs).all()
+        env.close()

@@ -263,3 +263,34 @@ def test_asmc_simple_step_info_matches_reference(golden):
         alive &= ~(g["terminated"][:, t] | g["truncated"][:, t])
         if not alive.any():
             break
+
+
+# --------------------------------------------------------------------------- round-4 fixtures
+@pytest.mark.parametrize("perturb", [False, True], ids=["plain", "perturb"])
+def test_asmc_highspeed_steps_match_reference(golden, perturb):
+    """usv-asmc-simple from injected states outside the action space's low-speed regime
+    (make_golden.py gen_asmc_highspeed): |u| > 1.2 hydrodynamics (usv_asmc.py:95-99), headings to
+    400 rad, adaptive gains to 5, u_d to 10; with and without do_perturb (:184-199)."""
+    from asmc_fixture import asmc_state, oracle_env
+    g = golden("asmc_highspeed.npz")
+    idx = np.flatnonzero(g["perturb"] == perturb)
+    e = oracle_env(g, idx, perturb)
+    elapsed = g["inj_elapsed"][idx].copy()
+    alive = np.ones(len(idx), bool)
+    for t in range(g["actions"].shape[1]):
+        o, r, te, tr = e.step(g["actions"][idx, t])
+        elapsed += 1
+        tr = tr | (elapsed >= 1000)
+        m = alive
+        np.testing.assert_array_equal(te[m], g["terminated"][idx][m, t], err_msg=f"t={t}")
+        np.testing.assert_array_equal(tr[m], g["truncated"][idx][m, t], err_msg=f"t={t}")
+        np.testing.assert_allclose(o[m], g["final_obs"][idx][m, t], rtol=1e-6, atol=1e-6, err_msg=f"t={t}")
+        np.testing.assert_allclose(r[m], g["reward"][idx][m, t], rtol=1e-9, atol=1e-9, err_msg=f"t={t}")
+        np.testing.assert_allclose(e.info["position"][m], g["info_position"][idx][m, t], rtol=1e-10, atol=1e-10)
+        np.testing.assert_allclose(e.info["velocity"][m], g["info_velocity"][idx][m, t], rtol=1e-10, atol=1e-10)
+        ref = asmc_state(g["so_out"][idx][m, t], g["last_out"][idx][m, t], g["aux_out"][idx][m, t])
+        np.testing.assert_allclose(e.asmc.state[m], ref, rtol=1e-9, atol=1e-9, err_msg=f"t={t}")
+        alive &= ~(g["terminated"][idx][:, t] | g["truncated"][idx][:, t])
+    # the regime this fixture exists for is actually reached
+    assert (e.asmc.fast_substeps > 0).sum() >= len(idx) // 3, e.asmc.fast_substeps
+    assert np.abs(g["inj_position"][idx, 2]).max() > 300
