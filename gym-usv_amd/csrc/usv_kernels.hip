@@ -560,16 +560,12 @@ __global__ __launch_bounds__(kBlock) void asmc_compute_kernel(int n, const R* __
 }
 
 // --------------------------------------------------------------------------- phase 1
-// UsvSimpleEnv.step kinematics..reward terms (simple_env.py:310-346); for usv-asmc-simple
-// first 2x UsvAsmc.compute (simple_env_asmc.py:18-27) and then step(zeros(2)).
-// Also returns sin/cos of the new heading so the wave-per-env lidar does not recompute them.
-template <typename R, int MODE>
-__device__ void env_dynamics(const State<R>& S, int e, float a_u, float a_r, float (&hdr)[kHdr],
-                             R& px, R& py, R& psp, R& pcp, R& partial, bool& trunc, R* info = nullptr) {
-  R x = S.F(F_X)[e], y = S.F(F_Y)[e], psi = S.F(F_PSI)[e];
-  R u = S.F(F_U)[e], v = S.F(F_V)[e], r = S.F(F_R)[e];
-  const int el0 = S.I(I_ELAPSED)[e];
-  if (MODE == USV_MODE_ASMC_SIMPLE) {
+// usv-asmc-simple's two UsvAsmc.compute calls (simple_env_asmc.py:19-25, usv_asmc.py:53-244) on env
+// e's pose and velocity, in registers; the ASMC state is loaded and stored here.
+template <typename R>
+__device__ __forceinline__ void asmc_env_chain(const State<R>& S, int e, int el0, float a_u, float a_r, R& x,
+                                               R& y, R& psi, R& u, R& v, R& r) {
+  {
     R s[kAsmcN];
 #pragma unroll
     for (int i = 0; i < kAsmcN; ++i) s[i] = S.asmc[(size_t)i * S.N + e];
@@ -600,6 +596,22 @@ __device__ void env_dynamics(const State<R>& S, int e, float a_u, float a_r, flo
     }
 #pragma unroll
     for (int i = 0; i < kAsmcN; ++i) S.asmc[(size_t)i * S.N + e] = s[i];
+  }
+}
+
+// UsvSimpleEnv.step kinematics..reward terms (simple_env.py:310-346); for usv-asmc-simple
+// first 2x UsvAsmc.compute (simple_env_asmc.py:18-27) and then step(zeros(2)).
+// Also returns sin/cos of the new heading so the wave-per-env lidar does not recompute them.
+// CHAIN = false (usv-asmc-simple only): asmc_chain_kernel already ran the two compute() calls and
+// stored the pose and velocity they left; this is then UsvSimpleEnv.step(zeros(2)) on them.
+template <typename R, int MODE, bool CHAIN = true>
+__device__ void env_dynamics(const State<R>& S, int e, float a_u, float a_r, float (&hdr)[kHdr],
+                             R& px, R& py, R& psp, R& pcp, R& partial, bool& trunc, R* info = nullptr) {
+  R x = S.F(F_X)[e], y = S.F(F_Y)[e], psi = S.F(F_PSI)[e];
+  R u = S.F(F_U)[e], v = S.F(F_V)[e], r = S.F(F_R)[e];
+  const int el0 = S.I(I_ELAPSED)[e];
+  if (MODE == USV_MODE_ASMC_SIMPLE) {
+    if constexpr (CHAIN) asmc_env_chain<R>(S, e, el0, a_u, a_r, x, y, psi, u, v, r);
     a_u = 0.0f;                                                                   // step(zeros(2))
     a_r = 0.0f;
   }
@@ -1886,7 +1898,8 @@ static_assert(4 * lds_q_bytes<kQE_S, kQW_S>() <= 160 * 1024, "four small blocks 
 // DONE: also write the done mask (io.done, ABI v4).  A template switch rather than a runtime test:
 // the raw step (usv_step, io.done null) then carries neither the pointer nor its branch in the pair
 // loop, whose SGPR budget is at its limit (a runtime test cost 0.25 us per launch).
-template <int MODE, bool FUSED, bool DONE = false, int kQE = ::usv::kQE, int kQW = ::usv::kQW>
+// CHAIN = false (usv-asmc-simple, FUSED): asmc_chain_kernel ran the ASMC chain, phase 1 the rest.
+template <int MODE, bool FUSED, bool DONE = false, int kQE = ::usv::kQE, int kQW = ::usv::kQW, bool CHAIN = true>
 __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<float>& io) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
@@ -1940,8 +1953,8 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
       float hdr[kHdr];
       float px, py, sp, cp, partial;
       bool trunc;
-      env_dynamics<float, MODE>(S, e, a.x, a.y, hdr, px, py, sp, cp, partial, trunc,
-                                io.info ? io.info + (size_t)e * USV_INFO_DIM : nullptr);
+      env_dynamics<float, MODE, CHAIN>(S, e, a.x, a.y, hdr, px, py, sp, cp, partial, trunc,
+                                       io.info ? io.info + (size_t)e * USV_INFO_DIM : nullptr);
       io.trunc[e] = trunc;
       make_qrec(recs + k * kQRec, px, py, sp, cp, partial, S.I(I_NOBS)[e], trunc, hdr);
     }
@@ -2079,12 +2092,12 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
   USV_STAMP_W(6);
 }
 
-template <int MODE, bool FUSED, bool DONE>
+template <int MODE, bool FUSED, bool DONE, bool CHAIN = true>
 __global__ __launch_bounds__(kQW * kWave) __attribute__((amdgpu_num_sgpr(USV_QSGPR), amdgpu_waves_per_eu(USV_QWPE, USV_QWPE)))
-void step_q_kernel(State<float> S, IO<float> io) { step_q_body<MODE, FUSED, DONE>(S, io); }
-template <int MODE, bool DONE>
+void step_q_kernel(State<float> S, IO<float> io) { step_q_body<MODE, FUSED, DONE, kQE, kQW, CHAIN>(S, io); }
+template <int MODE, bool DONE, bool CHAIN = true>
 __global__ __launch_bounds__(kQW_S * kWave) __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8)))
-void step_qs_kernel(State<float> S, IO<float> io) { step_q_body<MODE, true, DONE, kQE_S, kQW_S>(S, io); }
+void step_qs_kernel(State<float> S, IO<float> io) { step_q_body<MODE, true, DONE, kQE_S, kQW_S, CHAIN>(S, io); }
 
 // Split block-queue step, first half: full-width lane-per-env dynamics writing the env records
 // (make_qrec) for step_q_kernel<MODE, false, DONE>, plus truncated and the info row.
@@ -2100,6 +2113,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 2))) 
                             io.info ? io.info + (size_t)e * USV_INFO_DIM : nullptr);
   io.trunc[e] = trunc;
   make_qrec(S.qrec + (size_t)e * kQRec, px, py, sp, cp, partial, S.I(I_NOBS)[e], trunc, hdr);
+}
+
+// usv-asmc-simple, split at the ASMC chain (kind 6): the two UsvAsmc.compute calls of every env,
+// lane per env, pose and velocity stored back; step_q_kernel<ASMC_SIMPLE, true, DONE, false> then runs
+// UsvSimpleEnv.step(zeros(2)) on them in its fused phase 1.  The chain is a long dependent VALU
+// stream (one wave per SIMD at 65 536 envs); this kernel holds nothing else, so it carries no records,
+// headers or rewards, and the q kernel's phase 1 does that part at full width.
+template <typename R>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 2))) void asmc_chain_kernel(State<R> S, IO<R> io) {
+  const int e = blockIdx.x * kBlock + threadIdx.x;
+  if (e >= S.N) return;
+  const float2 a = reinterpret_cast<const float2*>(io.act)[e];
+  R x = S.F(F_X)[e], y = S.F(F_Y)[e], psi = S.F(F_PSI)[e];
+  R u = S.F(F_U)[e], v = S.F(F_V)[e], r = S.F(F_R)[e];
+  asmc_env_chain<R>(S, e, S.I(I_ELAPSED)[e], a.x, a.y, x, y, psi, u, v, r);
+  S.F(F_X)[e] = x; S.F(F_Y)[e] = y; S.F(F_PSI)[e] = psi;
+  S.F(F_U)[e] = u; S.F(F_V)[e] = v; S.F(F_R)[e] = r;
 }
 
 // --------------------------------------------------------------------------- reset kernel
@@ -2697,16 +2727,20 @@ void* pick_scan(int epw, int lid) {
   return pick_scan_lid<R, MODE, 4, WPB>(lid);
 }
 
+// split_chain (kind 6, usv-asmc-simple): the fused q kernel without the ASMC chain in its phase 1
 template <bool DONE>
-void* pick_q_done(int mode, bool fused, bool small) {
+void* pick_q_done(int mode, bool fused, bool small, bool split_chain) {
   const bool simple = mode == USV_MODE_SIMPLE;
+  if (!simple && split_chain)
+    return small ? (void*)&step_qs_kernel<USV_MODE_ASMC_SIMPLE, DONE, false>
+                 : (void*)&step_q_kernel<USV_MODE_ASMC_SIMPLE, true, DONE, false>;
   if (small) return simple ? (void*)&step_qs_kernel<USV_MODE_SIMPLE, DONE> : (void*)&step_qs_kernel<USV_MODE_ASMC_SIMPLE, DONE>;
   if (fused) return simple ? (void*)&step_q_kernel<USV_MODE_SIMPLE, true, DONE>
                            : (void*)&step_q_kernel<USV_MODE_ASMC_SIMPLE, true, DONE>;
   return simple ? (void*)&step_q_kernel<USV_MODE_SIMPLE, false, DONE> : (void*)&step_q_kernel<USV_MODE_ASMC_SIMPLE, false, DONE>;
 }
-void* pick_q(int mode, bool fused, bool small = false, bool done = false) {
-  return done ? pick_q_done<true>(mode, fused, small) : pick_q_done<false>(mode, fused, small);
+void* pick_q(int mode, bool fused, bool small = false, bool done = false, bool split_chain = false) {
+  return done ? pick_q_done<true>(mode, fused, small, split_chain) : pick_q_done<false>(mode, fused, small, split_chain);
 }
 
 template <typename R>
@@ -2754,15 +2788,18 @@ int launch_step_kernels(Handle* h, State<R>& S, const float* act, float* obs, vo
   const bool simple = h->cfg.mode == USV_MODE_SIMPLE;
   void* args[] = {(void*)&S, (void*)&io};
   if constexpr (std::is_same<R, float>::value) {
-    if (h->kind == 4 || h->kind == 5) {                     // block-queue step, kQE envs per block
+    if (h->kind == 4 || h->kind == 5 || h->kind == 6) {     // block-queue step, kQE envs per block
       if (h->kind == 4) {
         void* dyn = simple ? (void*)&dyn_rec_kernel<USV_MODE_SIMPLE> : (void*)&dyn_rec_kernel<USV_MODE_ASMC_SIMPLE>;
         HIP_TRY(hipLaunchKernel(dyn, dim3((S.N + kBlock - 1) / kBlock), dim3(kBlock), args, 0, st));
       }
-      const bool small = h->kind == 5 && h->epb == kQE_S;
+      if (h->kind == 6)                                      // usv-asmc-simple: the ASMC chain first
+        HIP_TRY(hipLaunchKernel((void*)&asmc_chain_kernel<float>, dim3((S.N + kBlock - 1) / kBlock), dim3(kBlock), args, 0, st));
+      const bool small = h->kind != 4 && h->epb == kQE_S;
       const int qe = small ? kQE_S : kQE, qw = small ? kQW_S : kQW;
-      HIP_TRY(hipLaunchKernel(pick_q(h->cfg.mode, h->kind == 5, small, io.done != nullptr), dim3((S.N + qe - 1) / qe), dim3(qw * kWave),
-                              args, small ? lds_q_bytes<kQE_S, kQW_S>() : lds_q_bytes(), st));
+      HIP_TRY(hipLaunchKernel(pick_q(h->cfg.mode, h->kind != 4, small, io.done != nullptr, h->kind == 6),
+                              dim3((S.N + qe - 1) / qe), dim3(qw * kWave), args,
+                              small ? lds_q_bytes<kQE_S, kQW_S>() : lds_q_bytes(), st));
       return USV_OK;
     }
   }
@@ -2973,12 +3010,13 @@ int set_experiment(Handle* h, State<R>& S, const usv_experiment* x) {
 
 // The block-queue step's LDS exceeds the 64 KiB default: raise the kernels' dynamic-LDS limit.
 int queue_lds_attr(const Handle* h) {
-  if (h->kind != 4 && h->kind != 5) return USV_OK;
+  if (h->kind != 4 && h->kind != 5 && h->kind != 6) return USV_OK;
+  const bool split = h->kind == 6;
   for (const bool done : {false, true}) {
-    HIP_TRY(hipFuncSetAttribute(pick_q(h->cfg.mode, h->kind == 5, false, done),
+    HIP_TRY(hipFuncSetAttribute(pick_q(h->cfg.mode, h->kind != 4, false, done, split),
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_q_bytes()));
-    if (h->kind == 5)
-      HIP_TRY(hipFuncSetAttribute(pick_q(h->cfg.mode, true, true, done), hipFuncAttributeMaxDynamicSharedMemorySize,
+    if (h->kind != 4)
+      HIP_TRY(hipFuncSetAttribute(pick_q(h->cfg.mode, true, true, done, split), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)lds_q_bytes<kQE_S, kQW_S>()));
   }
   return USV_OK;
@@ -3088,7 +3126,9 @@ int usv_create(const usv_config* cfg, int32_t device, void** out) {
     // (72.0 us at 65 536 envs against 77.4 at 4); block-wide dynamics (kind 3) spill the f64 ASMC
     // state at 4 waves per SIMD (94 us)
     const bool f64w = cfg->precision == USV_F64 && cfg->lidar_algo == USV_LIDAR_WINDOW && cfg->obstacle_cap <= 32;
-    if (queue) { h->kind = 4; h->epb = kQE; }
+    // f32 (window lidar, cap <= 32): the ASMC chain in its own launch, then the fused block-queue step
+    // with usv-simple's phase 1 (kind 6), small blocks below kQSmallBelow envs
+    if (queue) { h->kind = 6; h->epb = cfg->num_envs < kQSmallBelow ? kQE_S : kQE; }
     else if (f64w) { h->kind = 2; h->epb = cfg->num_envs >= 49152 ? 64 : 32; }
     else { h->kind = 2; h->epb = 16; }
   } else if (queue) {
@@ -3100,7 +3140,7 @@ int usv_create(const usv_config* cfg, int32_t device, void** out) {
     // at 65 536 envs: 40.3 us, against 47.7 for the split dyn_kernel + scan), else 8
     h->kind = 3; h->epb = cfg->num_envs >= 49152 ? 64 : 32;
   } else { h->kind = 1; h->epb = 64; }
-  h->prio = (h->kind == 4 || h->kind == 5) ? 0 : 1;   // the ramp helps static splits only
+  h->prio = h->kind >= 4 ? 0 : 1;      // the ramp helps static splits only
   if (const int rc = queue_lds_attr(h); rc != USV_OK) { delete h; return rc; }
   const int rc = cfg->precision == USV_F32 ? carve<float>(h, h->sf) : carve<double>(h, h->sd);
   if (rc != USV_OK) {
@@ -3123,7 +3163,8 @@ int usv_set_kernel_variant(void* hp, int32_t kind, int32_t epb, int32_t lid) {
                                       (epb == 64 && lid == 7 && cfg->precision == USV_F64)) && lid_ok;
   const bool blockdyn_ok = kind == 3 && (epb == 32 || epb == 64) && lid == 7 && cfg->precision == USV_F64 &&
                            cfg->mode == USV_MODE_SIMPLE;
-  const bool queue_ok = (kind == 4 || kind == 5) && (epb == kQE || (kind == 5 && epb == kQE_S)) && lid == 7 &&
+  const bool queue_ok = (kind == 4 || kind == 5 || (kind == 6 && cfg->mode == USV_MODE_ASMC_SIMPLE)) &&
+                        (epb == kQE || (kind != 4 && epb == kQE_S)) && lid == 7 &&
                         cfg->precision == USV_F32 && cfg->obstacle_cap <= 32;
   if (!(wave_ok || split_ok || blockdyn_ok || queue_ok)) return fail(USV_ERR_ARG, "kernel variant not available for this config");
   DeviceGuard g(h->device);
@@ -3135,7 +3176,7 @@ int usv_set_kernel_variant(void* hp, int32_t kind, int32_t epb, int32_t lid) {
   h->kind = kind;
   h->epb = epb;
   h->lid = lid;
-  h->prio = (kind == 4 || kind == 5) ? 0 : 1;
+  h->prio = kind >= 4 ? 0 : 1;
   return USV_OK;
 }
 

@@ -342,6 +342,8 @@ def test_step_variants_bit_identical(env_id, precision):
             + torch.tensor([0.2, -1.0], device="cuda") for _ in range(T)]
     ref = None
     queue = ("128,7,4", "128,7,5", "16,7,5") if precision == "f32" else ()   # block queue: f32 only
+    if precision == "f32" and env_id == "usv-asmc-simple":
+        queue += ("128,7,6", "16,7,6")                # ASMC chain kernel + fused block queue
     if precision == "f64":                            # f64: split scan at 16 envs/wave; block-wide dynamics
         queue = ("64,7,2", "64,7,3", "32,7,3") if env_id == "usv-simple" else ("64,7,2",)
     for v in ("64,7,1", "32,0,1", "32,3,1", "16,7,1", "32,7,1", "16,0,2", "32,3,2", "8,7,2", "16,7,2", "32,7,2") + queue:

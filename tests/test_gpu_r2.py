@@ -470,7 +470,9 @@ def test_two_process_sharding_bit_identical():
     ("usv-simple", "f32", None, 8192),        # small block-queue step (kind 5, 16 envs on 8 waves)
     ("usv-simple", "f32", None, 65536),       # the headline 128-env / 16-wave block-queue step (kind 5)
     ("usv-simple", "f32", "128,7,5", 8192),   # the same kernel forced at a small count (ragged tail too)
-    ("usv-asmc-simple", "f32", None, 8192),   # split block-queue step (kind 4)
+    ("usv-asmc-simple", "f32", None, 8192),   # ASMC chain kernel + small block-queue step (kind 6)
+    ("usv-asmc-simple", "f32", None, 65536),  # the same with 128-env blocks (the usv-asmc-simple default)
+    ("usv-asmc-simple", "f32", "128,7,4", 8192),   # split block-queue step (kind 4)
     ("usv-simple", "f32", "16,7,2", 8192),    # split wave scan (kind 2): vm_wait<2|4>
     ("usv-simple", "f64", None, 8192),        # f64 block-wide dynamics + wave scan (kind 3, 8 envs/wave)
     ("usv-simple", "f64", None, 65536),       # the same at 16 envs/wave (the f64 default at C3)

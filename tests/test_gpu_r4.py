@@ -213,3 +213,31 @@ def test_unseeded_single_env_reset(env_id):
         obs = out if env_id != "usv-simple" else out[0]
         assert np.isfinite(obs).all()
         env.close()
+
+
+@pytest.mark.parametrize("n", [1, 77, 1077, 40000])
+def test_asmc_split_chain_bit_identical(n):
+    """usv-asmc-simple kind 6 (asmc_chain_kernel, then the fused block-queue step running
+    UsvSimpleEnv.step(zeros(2)) in its phase 1; both block shapes) against the fused wave kernel
+    and the split block queue (kind 4), over a rollout with TimeLimit resets and ragged env counts:
+    bitwise equal outputs, terminal rows and info rows."""
+    T = 30
+    gen = torch.Generator(device="cuda").manual_seed(8)
+    acts = [torch.rand(n, 2, device="cuda", generator=gen) * torch.tensor([0.8, 2.0], device="cuda")
+            + torch.tensor([0.2, -1.0], device="cuda") for _ in range(T)]
+    ref = None
+    for v in ("64,7,1", "128,7,4", "128,7,6", "16,7,6", None):
+        env = make("usv-asmc-simple", n, seed=6, max_episode_steps=11, kernel_variant=v, copy=False, info=True)
+        env.reset(seed=6)
+        outs = []
+        for a in acts:
+            o, r, te, tr, info = env.step(a)
+            outs.append([x.clone() for x in (o, r, te, tr, info["final_obs"], info["position"], info["ye_reward"])])
+        outs.append([torch.from_numpy(env.get_field("asmc"))])
+        env.close()
+        if ref is None:
+            ref = outs
+            continue
+        for t, (a_, b_) in enumerate(zip(ref, outs)):
+            for x, y in zip(a_, b_):
+                assert torch.equal(x, y), f"variant {v} differs at step {t} (n={n})"
