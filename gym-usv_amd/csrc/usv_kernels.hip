@@ -126,6 +126,17 @@ __device__ __forceinline__ void qprof_flush(QProf*) {}
 template <typename T> __device__ __forceinline__ void st_out(T* p, T v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // global_store ... sc1
 }
+// obs-row stores of the block-queue step (diagnostic builds: -DUSV_OBS_PLAIN for plain stores)
+template <typename T> __device__ __forceinline__ void st_obs(T* p, T v) {
+#ifdef USV_OBS_PLAIN
+  *p = v;
+#else
+  st_out(p, v);
+#endif
+}
+#ifndef USV_ROW_STORE
+#define USV_ROW_STORE 1    // 1: pair spans from 32-B sectors (round 4); 0: per-row pieces (round 3)
+#endif
 // Division and square root of the per-step dynamics: in the f32 build the hardware reciprocal and
 // square root (1 ulp; the reference's float64 values are matched to SURVEY 8(c)'s tolerance), which
 // shortens the dependent chain of the block queue's phase 1 (barrier exit 3.4 -> 2.6 us); IEEE in
@@ -1007,9 +1018,14 @@ __device__ __forceinline__ void lidar_window(float dx, float dy, float key, floa
 // r / sin(61 deg), or the boat inside it) take all 128 rays, the exact test sorting them out.
 // `far` (wave-uniform): some obstacle is >= 99 m away, where the reference's `< max range` test
 // (usv_asmc_ca_env.py:458) can matter; it is applied to every pair then.
+// rotA / rotB (wave-uniform, 0..63): lane l receives env A's readings of rays (l - rotA) & 63 and
+// 64 + ((l - rotA) & 63) (env B likewise with rotB), i.e. the scan rotated across lanes for free (the
+// slot reads take the rotated addresses); the block-queue step stores an env pair's obs rows as
+// 32-B-aligned spans this way.
 __device__ __forceinline__ void lidar_window2(float dx, float dy, float key, float d, float rr, bool valid, bool far,
                                               float c0r, float s0r, float4* rec, const WinLds& L, int* mark2,
-                                              Scan<float>& A, Scan<float>& B, QProf* qp = nullptr) {
+                                              Scan<float>& A, Scan<float>& B, QProf* qp = nullptr,
+                                              int rotA = 0, int rotB = 0) {
   const int l = lane_id();
   float a, b;
   to_ray0(dx, dy, c0r, s0r, a, b);
@@ -1105,9 +1121,11 @@ __device__ __forceinline__ void lidar_window2(float dx, float dy, float key, flo
   QMARK(3);
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");     // all lanes' ds_min_u64 landed
   __builtin_amdgcn_wave_barrier();
-  const unsigned long long a0 = L.slot[l], a1s = L.slot[l + 64];
-  const unsigned long long b0 = L.slot[128 + l], b1s = L.slot[192 + l];
-  L.slot[l] = kSlotArm; L.slot[l + 64] = kSlotArm;    // re-arm for this wave's next pair
+  const int la = (l - rotA) & (kWave - 1), lb = (l - rotB) & (kWave - 1);
+  const unsigned long long a0 = L.slot[la], a1s = L.slot[la + 64];
+  const unsigned long long b0 = L.slot[128 + lb], b1s = L.slot[192 + lb];
+  // re-arm for this wave's next pair (after every lane's reads: a wave's LDS ops complete in order)
+  L.slot[l] = kSlotArm; L.slot[l + 64] = kSlotArm;
   L.slot[128 + l] = kSlotArm; L.slot[192 + l] = kSlotArm;
   L.mark[l] = 0;
   A.rd0 = __uint_as_float((unsigned)a0);              // no hit: the armed payload, max range
@@ -1123,7 +1141,7 @@ __device__ __forceinline__ void lidar_window2(float dx, float dy, float key, flo
 __device__ __forceinline__ void lidar_wave2(float* rows, int os, int nl, float px, float py, float c0r,
                                             float s0r, const float2* rayoff, unsigned long long* slot,
                                             int* mark, int* mark2, Scan<float>& A, Scan<float>& B,
-                                            QProf* qp = nullptr) {
+                                            QProf* qp = nullptr, int rotA = 0, int rotB = 0) {
   const int l = lane_id();
   const int jl = l & 31;
   const bool valid = jl < nl;
@@ -1142,7 +1160,7 @@ __device__ __forceinline__ void lidar_wave2(float* rows, int os, int nl, float p
   A.far = B.far = false;
   const bool far = (vm & ballot(d >= (float)(0.99 * kSensorMax))) != 0;
   lidar_window2(dx, dy, key, d, rr, valid, far, c0r, s0r, reinterpret_cast<float4*>(rows), WinLds{slot, mark, rayoff},
-                mark2, A, B, qp);
+                mark2, A, B, qp, rotA, rotB);
 }
 
 // Angular-window lidar for the f64 build (one env per wave).  The ray windows are sized in float from
@@ -1865,19 +1883,21 @@ __device__ __forceinline__ float qrec_hdr(const float* rec, int i) {
 }
 
 // Terminal obs and stale scan of a done env e (rare path; lane l holds its rays l, l + 64).
+// `rot`: the scan is rotated across lanes (lane l holds rays (l - rot) & 63 and 64 + that).
 __device__ __forceinline__ void q_emit_done(const State<float>& S, const IO<float>& io, int e,
-                                            const Scan<float>& sc, const float* rec) {
+                                            const Scan<float>& sc, const float* rec, int rot) {
   const int l = lane_id();
+  const int ray = (l - rot) & (kWave - 1);
   if (io.fobs) {
     float* f = io.fobs + (size_t)e * kObsDim;
-    f[kHdr + l] = l_norm(sc.rd0);
-    f[kHdr + 64 + l] = l_norm(sc.rd1);
+    f[kHdr + ray] = l_norm(sc.rd0);
+    f[kHdr + 64 + ray] = l_norm(sc.rd1);
     const int hi = min(l, kHdr - 1);
     f[hi] = qrec_hdr(rec, hi);
   }
   if (S.autoreset == USV_AUTORESET_SAME_STEP) {
-    S.sensor_last[(size_t)e * kSensors + l] = sc.rd0;
-    S.sensor_last[(size_t)e * kSensors + 64 + l] = sc.rd1;
+    S.sensor_last[(size_t)e * kSensors + ray] = sc.rd0;
+    S.sensor_last[(size_t)e * kSensors + 64 + ray] = sc.rd1;
   }
 }
 
@@ -1975,27 +1995,28 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
   // inside it their registers would spill the loop's to scratch
   int it = 0;
   const bool hb = l >= 32;
-  // obs-header lanes (loop-invariant, packed in one register): lanes 0..14 store env A's header
-  // value hi, 15..29 env B's, 30..63 repeat lane 29; the record slot of value hi (qrec_hdr) in bits
-  // 8..12, bit 16: env B's lane, bit 17: a constant entry (1, 10, 12, 13, 14)
-  int hpk;
-  {
-    const int hl = min(l, 2 * kHdr - 1);
-    const int hi = hl >= kHdr ? hl - kHdr : hl;
-    const int hrec = hi == 0 ? 6 : (hi <= 9 ? hi + 5 : 15);
-    hpk = hi | (hrec << 8) | ((hl >= kHdr) << 16) | ((hi == 1 || hi == 10 || hi >= 12) << 17);
-  }
   auto pair_hasb = [&](int p) { return 2 * p + 1 < nbe; };
+  // An env pair's two obs rows are one 1144-B span, stored as five 256-B wave stores from the span's
+  // first 32-B sector: every sector but the two at the span's ends is written whole by one write-through
+  // store (the four sensor halves and the header store of round 3 split ~3 sectors per row between
+  // instructions, 1.18x the algorithmic write bytes).  sh = the span's dword offset in its sector.
+  const unsigned ob = (unsigned)(((uintptr_t)io.obs >> 2) & 7);
+  auto pair_shift = [&](int p) { return (int)((ob + (unsigned)(eb + 2 * p) * (unsigned)kObsDim) & 7u); };
   // env record of pair c for this lane (lanes 0..31 env A, 32..63 env B; env A again when there is
-  // no B): pose, meta and the obs-header value this lane stores.  Read one pair ahead (after the
-  // current pair's scan), so the LDS latency overlaps the current pair's stores.
+  // no B): pose, meta and the obs-header value this lane stores (lanes sh..sh+14: env A's entries
+  // 0..14, sh+15..sh+29: env B's; no env B: sh = 0 and lanes 15..29 repeat env A's).  Read one pair
+  // ahead (after the current pair's scan), so the LDS latency overlaps the current pair's stores.
   auto rec_of = [&](int c, float4& P, float4& M, float& H) {
     const int c0 = 2 * c;
     const bool cB = pair_hasb(c);
     const float* const rk = recs + ((hb && cB) ? c0 + 1 : c0) * kQRec;
     P = *reinterpret_cast<const float4*>(rk);
     M = *reinterpret_cast<const float4*>(rk + 4);
-    H = recs[((((hpk >> 16) & 1) && cB) ? c0 + 1 : c0) * kQRec + ((hpk >> 8) & 31)];
+    const int hl = min(max(l - ((USV_ROW_STORE && cB) ? pair_shift(c) : 0), 0), 2 * kHdr - 1);
+    const int hi = hl >= kHdr ? hl - kHdr : hl;
+    const float v = recs[((hl >= kHdr && cB) ? c0 + 1 : c0) * kQRec + (hi == 0 ? 6 : (hi <= 9 ? hi + 5 : 15))];
+    H = (hi == 1 || hi == 10 || hi == 13) ? 0.0f                  // make_header's constant entries
+      : hi == 12 ? (float)(kMaxAccU / 10.0) : hi == 14 ? (float)(kMaxAccR / 10.0) : v;
   };
   for (;;) {
     unsigned done = 0;
@@ -2020,16 +2041,18 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
       const int kl = (hb && hasB) ? k0 + 1 : k0;
       const int el = e0 + (kl - k0);
       const int nt = __float_as_int(meta.y);
+      // the pair's span offset and the lane rotations of the two scans that put each reading in the
+      // lane that stores it (no env B: the rows are stored as in round 3, unrotated)
+      const bool span2 = USV_ROW_STORE && hasB;
+      const int sh = span2 ? pair_shift(cur) : 0;
+      const int rotA = span2 ? kHdr + sh : 0, rotB = span2 ? 2 * kHdr + sh : 0;
       Scan<float> sa, sb;
       QMARK(1);
       lidar_wave2(cbuf, os, (hb && !hasB) ? 0 : (nt & 0xffff), pose.x, pose.y, pose.z, pose.w, rayoff, slot,
-                  mark, reinterpret_cast<int*>(nbuf) + 192, sa, sb, qp);
+                  mark, reinterpret_cast<int*>(nbuf) + 192, sa, sb, qp, rotA, rotB);
       float4 pose_n = pose, meta_n = meta;
       float hv_n = hv;
       if (nxt >= 0) rec_of(nxt, pose_n, meta_n, hv_n);   // the next pair's record (wave-uniform)
-      // env B's outputs (env A's again when there is none: identical stores to the same addresses
-      // keep every memory instruction of the loop non-divergent and its count static)
-      const float sB0 = hasB ? sb.rd0 : sa.rd0, sB1 = hasB ? sb.rd1 : sa.rd1;
       // collision (:153-156): two compares and ballots per env (a fminf of the two readings would
       // canonicalise both first)
       const float kc = (float)kCollDist;
@@ -2037,16 +2060,28 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
       const bool collB = hasB ? (ballot(sb.rd0 < kc) | ballot(sb.rd1 < kc)) != 0 : collA;
       const bool termB = hasB ? sb.term : sa.term;
       float* const rowA = io.obs + (size_t)e0 * kObsDim;
-      float* const rowB = rowA + (hasB ? kObsDim : 0);
-      st_out(rowA + kHdr + l, l_norm(sa.rd0));          // sensors (:82-83)
-      st_out(rowA + kHdr + 64 + l, l_norm(sa.rd1));
-      st_out(rowB + kHdr + l, l_norm(sB0));
-      st_out(rowB + kHdr + 64 + l, l_norm(sB1));
-      {                                                 // headers: lanes 0..14 env A, 15..29 env B
-        const int hi = hpk & 31;
-        const bool hB = ((hpk >> 16) & 1) && hasB;      // (no env B: env A's value again)
-        const float hc = hi == 12 ? (float)(kMaxAccU / 10.0) : hi == 14 ? (float)(kMaxAccR / 10.0) : 0.0f;
-        st_out(rowA + (hB ? kObsDim : 0) + hi, ((hpk >> 17) & 1) ? hc : hv);
+      // the obs rows (header :91-96, sensors :82-83): five stores either way, so the loop's count of
+      // memory instructions stays static (vm_wait below)
+      if (span2) {
+        // span dword 64 j + l - sh = lane l of store j: [header A | sensors A | header B | sensors B]
+        float* const span = rowA - sh;
+        const float a0 = l_norm(sa.rd0), a1 = l_norm(sa.rd1), b0 = l_norm(sb.rd0), b1 = l_norm(sb.rd1);
+        const bool mA = l < kHdr + sh, mB = l < 2 * kHdr + sh;
+        if (l >= sh) st_obs(span + l, mA ? hv : a0);   // (lanes < sh: the previous pair's dwords)
+        st_obs(span + 64 + l, mA ? a0 : a1);
+        st_obs(span + 128 + l, mA ? a1 : (mB ? hv : b0));
+        st_obs(span + 192 + l, mB ? b0 : b1);
+        if (mB) st_obs(span + 256 + l, b1);             // (lanes >= 30 + sh: the next pair's)
+      } else {
+        // per-row pieces: each row's sensors in two 256-B stores and the two headers in one (a lone
+        // env, odd env count: env A's row twice, identical values to identical addresses)
+        float* const rowB = rowA + (hasB ? kObsDim : 0);
+        st_obs(rowA + kHdr + l, l_norm(sa.rd0));
+        st_obs(rowA + kHdr + 64 + l, l_norm(sa.rd1));
+        st_obs(rowB + kHdr + l, l_norm(hasB ? sb.rd0 : sa.rd0));
+        st_obs(rowB + kHdr + 64 + l, l_norm(hasB ? sb.rd1 : sa.rd1));
+        const int hl = min(l, 2 * kHdr - 1);           // lanes 0..14 env A, 15..29 env B (or A again)
+        st_obs((hl >= kHdr ? rowB - kHdr : rowA) + hl, hv);
       }
       const bool term_l = hb ? termB : sa.term;         // reward, terminated: lanes 0..31 env A,
       const bool coll_l = hb ? collB : collA;           // 32..63 env B
@@ -2057,8 +2092,8 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
       const unsigned long long dm = ballot(done_l);
       const bool doneA = (unsigned)dm != 0u, doneB = hasB && (unsigned)(dm >> 32) != 0u;
       if (doneA | doneB) {
-        if (doneA) q_emit_done(S, io, e0, sa, recs + k0 * kQRec);
-        if (doneB) q_emit_done(S, io, e0 + 1, sb, recs + (k0 + 1) * kQRec);
+        if (doneA) q_emit_done(S, io, e0, sa, recs + k0 * kQRec, rotA);
+        if (doneB) q_emit_done(S, io, e0 + 1, sb, recs + (k0 + 1) * kQRec, rotB);
       }
       // the next pair's rows landed: at least seven stores (four sensor halves, the headers, the
       // rewards and the terminated flags) were issued after their DMA

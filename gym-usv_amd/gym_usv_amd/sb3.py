@@ -24,7 +24,12 @@ restated from SB3 2.x:
 * ``frame_stack=k`` is ``VecFrameStack(k)`` (channels-last: the newest obs is the last block,
   a done env's stack is zeroed before the reset obs is pushed), computed on the device.
 
-The step itself stays on the GPU; only the arrays SB3 consumes are copied to the host.
+The step itself stays on the GPU; only the arrays SB3 consumes are copied to the host, into
+page-locked buffers: the stacked obs on a copy stream while the host builds the done envs' infos,
+the small arrays (reward, done) first, and the terminal rows of the done envs only.  The returned
+arrays alternate between two such buffer sets, so each stays valid until the second-next step
+(SB3's collectors consume or copy them within one step).  ``infos`` entries of envs that did not end
+are shared empty dicts (DummyVecEnv builds 4096 fresh ones per step: ~0.25 ms of Python).
 """
 from __future__ import annotations
 
@@ -109,9 +114,25 @@ class Sb3VecEnv:
         self._seed = seed
         self._actions = None
         dev = venv.device
-        self._ep_ret = torch.zeros(self.num_envs, dtype=torch.float64, device=dev)
-        self._ep_len = torch.zeros(self.num_envs, dtype=torch.int64, device=dev)
+        n = self.num_envs
+        self._ep_ret = torch.zeros(n, dtype=torch.float64, device=dev)
+        self._ep_len = torch.zeros(n, dtype=torch.int64, device=dev)
         self._t0 = time.time()
+        # host side: page-locked buffers (two sets, alternating) and a copy stream on a GPU
+        self._cuda = dev.type == "cuda"
+        pin = self._cuda
+        w = d * (frame_stack or 1)
+        self._host = [dict(obs=torch.empty((n, w), dtype=torch.float32, pin_memory=pin),
+                           rew=torch.empty(n, dtype=torch.float32, pin_memory=pin),
+                           done=torch.empty(n, dtype=torch.bool, pin_memory=pin)) for _ in range(2)]
+        self._hb = 0
+        self._act_host = torch.empty((n, venv.act_dim), dtype=torch.float32, pin_memory=pin)
+        self._act_dev = torch.empty((n, venv.act_dim), dtype=torch.float32, device=dev)
+        self._rew32 = torch.empty(n, dtype=torch.float32, device=dev)
+        self._copy_stream = torch.cuda.Stream(dev) if self._cuda else None
+        self._empty = [{} for _ in range(n)]           # infos of envs that did not end (shared)
+        self._infos = list(self._empty)
+        self._filled = np.empty(0, dtype=np.int64)
 
     # ---------------------------------------------------------------- VecEnv API
     def reset(self):
@@ -127,35 +148,69 @@ class Sb3VecEnv:
         self._actions = actions
 
     def step_wait(self):
-        a = torch.as_tensor(np.asarray(self._actions, dtype=np.float32), device=self.venv.device)
-        obs, rew, term, trunc, info = self.venv.step(a)
+        venv, n, dev = self.venv, self.num_envs, self.venv.device
+        np.copyto(self._act_host.numpy(), np.asarray(self._actions, dtype=np.float32).reshape(n, -1))
+        self._act_dev.copy_(self._act_host, non_blocking=self._cuda)
+        obs, rew, term, trunc, info = venv.step(self._act_dev)
         done = info["_final_obs"]                       # terminated | truncated, written by the step kernel
-        self._ep_ret += rew.to(torch.float64)
-        self._ep_len += 1
         final = info.get("final_obs")
-        term_stack = None
-        if self._stack is not None:
-            obs, term_stack = self._stack.step(obs, done, final)
-        # host copies (what SB3 consumes)
-        obs_np = obs.cpu().numpy()
-        rew_np = rew.to(torch.float32).cpu().numpy()
-        done_np = done.cpu().numpy()
-        infos = [{} for _ in range(self.num_envs)]
-        if done_np.any():
-            idx = np.flatnonzero(done_np)
-            tidx = torch.as_tensor(idx, device=self.venv.device)
-            term_obs = (term_stack if term_stack is not None else final[tidx]).cpu().numpy()
-            trunc_np = (trunc & ~term)[tidx].cpu().numpy()
-            ret = self._ep_ret[tidx].cpu().numpy()
-            length = self._ep_len[tidx].cpu().numpy()
+        self._ep_ret += rew
+        self._ep_len += 1
+        st = self._stack
+        old = None
+        if st is not None:
+            # VecFrameStack: roll by one obs, zero the done envs' stacks, push the new obs; `old` keeps
+            # the previous stacks for the done envs' terminal observations below
+            old, new, d = st.buf, st._bufs[1 - st._i], st.d
+            torch.mul(old[:, d:], (~done)[:, None], out=new[:, :-d])
+            new[:, -d:] = obs
+            st._i = 1 - st._i
+            obs = new
+        h = self._host[self._hb]
+        self._hb ^= 1
+        if self._cuda:
+            # the stacked obs (the big copy) on the copy stream, overlapping the rest of this call
+            ready = torch.cuda.Event()
+            ready.record()
+            cs = self._copy_stream
+            cs.wait_event(ready)
+            with torch.cuda.stream(cs):
+                h["obs"].copy_(obs, non_blocking=True)
+                obs_done = torch.cuda.Event()
+                obs_done.record(cs)
+            obs.record_stream(cs)
+            self._rew32.copy_(rew)
+            h["rew"].copy_(self._rew32, non_blocking=True)
+            h["done"].copy_(done, non_blocking=True)
+            small = torch.cuda.Event()
+            small.record()
+            small.synchronize()
+        else:
+            h["obs"].copy_(obs)
+            h["rew"].copy_(rew)
+            h["done"].copy_(done)
+        done_np = h["done"].numpy()
+        for i in self._filled:                          # last step's done envs: back to empty infos
+            self._infos[i] = self._empty[i]
+        idx = np.flatnonzero(done_np)
+        if idx.size:
+            ti = torch.from_numpy(idx).to(dev)
+            rows = final[ti] if old is None else torch.cat((old[ti, st.d:], final[ti]), dim=1)
+            w = rows.shape[1]
+            # one device->host copy: terminal rows, TimeLimit.truncated, episode return and length
+            pack = torch.cat((rows.to(torch.float64), (trunc & ~term)[ti, None].to(torch.float64),
+                              self._ep_ret[ti, None], self._ep_len[ti, None].to(torch.float64)), dim=1).cpu().numpy()
+            self._ep_ret[ti] = 0
+            self._ep_len[ti] = 0
             t = round(time.time() - self._t0, 6)
+            term_obs = pack[:, :w].astype(np.float32)
             for j, i in enumerate(idx):
-                infos[i]["terminal_observation"] = term_obs[j]
-                infos[i]["TimeLimit.truncated"] = bool(trunc_np[j])
-                infos[i]["episode"] = {"r": round(float(ret[j]), 6), "l": int(length[j]), "t": t}
-            self._ep_ret[tidx] = 0
-            self._ep_len[tidx] = 0
-        return obs_np, rew_np, done_np, infos
+                self._infos[i] = {"terminal_observation": term_obs[j], "TimeLimit.truncated": bool(pack[j, w]),
+                                  "episode": {"r": round(float(pack[j, w + 1]), 6), "l": int(pack[j, w + 2]), "t": t}}
+        self._filled = idx
+        if self._cuda:
+            obs_done.synchronize()
+        return h["obs"].numpy(), h["rew"].numpy(), done_np, list(self._infos)
 
     def step(self, actions):
         self.step_async(actions)

@@ -39,6 +39,11 @@ HS_TOL = {"f64": dict(hdr=2e-6, rew=1e-8, vel=1e-9, state=1e-9),
 @pytest.mark.parametrize("precision", ["f64", "f32"])
 @pytest.mark.parametrize("perturb", [False, True], ids=["plain", "perturb"])
 def test_asmc_highspeed_replay(golden, precision, perturb):
+    """Up to each env's first episode end.  The adaptive-gain derivatives Ka_dot_u / Ka_dot_psi
+    (usv_asmc.py:137-140) are switches (+-k, k_min): in f32 a sliding surface within rounding of
+    its threshold mu picks the other branch, after which that env follows another control law.
+    Such envs are counted (a branch-flip rate, bounded) and compared no further; the others
+    are held to the stated bounds."""
     g = golden("asmc_highspeed.npz")
     idx = np.flatnonzero(g["perturb"] == perturb)
     n, T = len(idx), g["actions"].shape[1]
@@ -46,37 +51,39 @@ def test_asmc_highspeed_replay(golden, precision, perturb):
     env.set_state(env_state(g, idx))
     orc = oracle_env(g, idx, perturb)           # the checker: counts the |u| > 1.2 substeps
     alive = np.ones(n, bool)
+    flipped = np.zeros(n, bool)
     worst = dict(hdr=0.0, rew=0.0, vel=0.0, pos=0.0, state=0.0)
     flips = rays = 0
-    orc_state = []
+    cont = np.array([k for k in range(16) if k not in (11, 12)])    # continuous state entries
     for t in range(T):
         a = torch.from_numpy(g["actions"][idx, t]).cuda()
         obs, rew, term, trunc, info = env.step(a)
         obs, rew, term, trunc, ipos, ivel = to_np(obs, rew, term, trunc, info["position"], info["velocity"])
         orc.step(g["actions"][idx, t])
-        orc_state.append(orc.asmc.state.copy())
-        m = alive
-        if not m.any():
-            break
-        ref = g["final_obs"][idx][m, t]
-        worst["hdr"] = max(worst["hdr"], float((np.abs(obs[m, :15] - ref[:, :15]) - 1e-4 * np.abs(ref[:, :15])).max()))
-        flips += int((np.abs(obs[m, 15:] - ref[:, 15:]) > 1e-5 + 1e-4 * np.abs(ref[:, 15:])).sum())
-        rays += int(m.sum()) * 128
-        worst["rew"] = max(worst["rew"], float(np.abs(rew[m] - g["reward"][idx][m, t]).max()))
-        rv = g["info_velocity"][idx][m, t]
-        worst["vel"] = max(worst["vel"], float((np.abs(ivel[m] - rv) / np.maximum(1, np.abs(rv))).max()))
-        rp = g["info_position"][idx][m, t]
-        worst["pos"] = max(worst["pos"], float((np.abs(ipos[m] - rp) / np.maximum(1, np.abs(rp))).max()))
         st = env.get_field("asmc")
-        rs = asmc_state(g["so_out"][idx][m, t], g["last_out"][idx][m, t], g["aux_out"][idx][m, t])
-        worst["state"] = max(worst["state"], float((np.abs(st[m] - rs) / np.maximum(1, np.abs(rs))).max()))
-        np.testing.assert_array_equal(term[m], g["terminated"][idx][m, t], err_msg=f"t={t}")
-        np.testing.assert_array_equal(trunc[m], g["truncated"][idx][m, t], err_msg=f"t={t}")
+        rs = asmc_state(g["so_out"][idx][:, t], g["last_out"][idx][:, t], g["aux_out"][idx][:, t])
+        flipped |= alive & (np.abs(st[:, [11, 12]] - rs[:, [11, 12]]) > 1e-6).any(axis=1)
+        m = alive & ~flipped
+        if m.any():
+            ref = g["final_obs"][idx][m, t]
+            worst["hdr"] = max(worst["hdr"], float((np.abs(obs[m, :15] - ref[:, :15]) - 1e-4 * np.abs(ref[:, :15])).max()))
+            flips += int((np.abs(obs[m, 15:] - ref[:, 15:]) > 1e-5 + 1e-4 * np.abs(ref[:, 15:])).sum())
+            rays += int(m.sum()) * 128
+            worst["rew"] = max(worst["rew"], float(np.abs(rew[m] - g["reward"][idx][m, t]).max()))
+            rv, rp = g["info_velocity"][idx][m, t], g["info_position"][idx][m, t]
+            worst["vel"] = max(worst["vel"], float((np.abs(ivel[m] - rv) / np.maximum(1, np.abs(rv))).max()))
+            worst["pos"] = max(worst["pos"], float((np.abs(ipos[m] - rp) / np.maximum(1, np.abs(rp))).max()))
+            d = np.abs(st[m][:, cont] - rs[m][:, cont]) / np.maximum(1, np.abs(rs[m][:, cont]))
+            worst["state"] = max(worst["state"], float(d.max()))
+            np.testing.assert_array_equal(term[m], g["terminated"][idx][m, t], err_msg=f"t={t}")
+            np.testing.assert_array_equal(trunc[m], g["truncated"][idx][m, t], err_msg=f"t={t}")
         alive &= ~(g["terminated"][idx][:, t] | g["truncated"][idx][:, t])
     fast = int(orc.asmc.fast_substeps.sum())
     print(f"\n[asmc highspeed {precision} perturb={perturb}] {fast} substeps with |u| > 1.2 over {n} envs; "
+          f"Ka-switch flips {int(flipped.sum())}/{n} envs; "
           + ", ".join(f"{k} {v:.2e}" for k, v in worst.items()) + f"; sensor flips {flips}/{rays}")
     assert fast > 0 and (orc.asmc.fast_substeps > 0).sum() >= n // 3
+    assert flipped.sum() <= (0 if precision == "f64" else max(2, n // 8)), flipped.sum()
     tol = HS_TOL[precision]
     assert worst["hdr"] <= tol["hdr"] and worst["rew"] <= tol["rew"], worst
     assert worst["vel"] <= tol["vel"] and worst["pos"] <= tol["vel"] and worst["state"] <= tol["state"], worst
