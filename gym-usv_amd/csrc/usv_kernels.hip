@@ -1865,6 +1865,22 @@ __device__ __forceinline__ void dma_copy1(const void* src, void* dst, int bytes)
   }
 }
 
+// dma_copy1 from a loop-invariant wave-uniform base (SGPR pair) at a wave-uniform byte offset `off`
+// carried in the lanes' 32-bit offsets: the pair loop then computes no 64-bit row address per pair.
+__device__ __forceinline__ void dma_copy_at(const void* base, int off, void* dst, int bytes) {
+  const int c = lane_id();
+  const unsigned d = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)dst);
+  const uint64_t a = (uint64_t)(uintptr_t)base;
+  const uint64_t sb = ((uint64_t)(unsigned)__builtin_amdgcn_readfirstlane((unsigned)(a >> 32)) << 32) |
+                      (uint64_t)(unsigned)__builtin_amdgcn_readfirstlane((unsigned)a);
+  if (c < bytes / 16) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\t"
+                 "global_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep) : "v"(16 * c + off), "s"(sb), "s"(d) : "memory");
+  }
+}
+
 __device__ __forceinline__ void make_qrec(float* rec, float px, float py, float sp, float cp, float partial,
                                           int n, bool trunc, const float (&h)[kHdr]) {
   const float c0 = ray_c(cp, sp, (float)kStartC, (float)kStartS), s0 = ray_s(cp, sp, (float)kStartC, (float)kStartS);
@@ -1996,6 +2012,7 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
   int it = 0;
   const bool hb = l >= 32;
   auto pair_hasb = [&](int p) { return 2 * p + 1 < nbe; };
+  const float* const oblk = S.orow(eb);               // this block's obstacle rows (pair p at 2 p rowb bytes)
   // An env pair's two obs rows are one 1144-B span, stored as five 256-B wave stores from the span's
   // first 32-B sector: every sector but the two at the span's ends is written whole by one write-through
   // store (the four sensor halves and the header store of round 3 split ~3 sectors per row between
@@ -2014,9 +2031,13 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
     M = *reinterpret_cast<const float4*>(rk + 4);
     const int hl = min(max(l - ((USV_ROW_STORE && cB) ? pair_shift(c) : 0), 0), 2 * kHdr - 1);
     const int hi = hl >= kHdr ? hl - kHdr : hl;
-    const float v = recs[((hl >= kHdr && cB) ? c0 + 1 : c0) * kQRec + (hi == 0 ? 6 : (hi <= 9 ? hi + 5 : 15))];
-    H = (hi == 1 || hi == 10 || hi == 13) ? 0.0f                  // make_header's constant entries
-      : hi == 12 ? (float)(kMaxAccU / 10.0) : hi == 14 ? (float)(kMaxAccR / 10.0) : v;
+    float v = recs[((hl >= kHdr && cB) ? c0 + 1 : c0) * kQRec + (hi == 0 ? 6 : (hi <= 9 ? hi + 5 : 15))];
+    // make_header's constant entries 1, 10, 13 (0) and 12, 14 (max_acceleration / 10), as selects:
+    // written as one conditional chain the compiler branches on exec around the record read
+    const bool cst = ((0x7402 >> hi) & 1) != 0;
+    const float hc = hi == 12 ? (float)(kMaxAccU / 10.0) : (hi == 14 ? (float)(kMaxAccR / 10.0) : 0.0f);
+    asm volatile("" : "+v"(v));
+    H = cst ? hc : v;
   };
   for (;;) {
     unsigned done = 0;
@@ -2035,7 +2056,11 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
       if (nxt >= np) nxt = -1;
       if (nxt >= 0) {                                  // wave-uniform
         if (l == 0) tk = atomicAdd(qctr, 1u);
+#ifdef USV_DMA_ROW64
         dma_copy1(S.orow(eb + 2 * nxt), nbuf, (pair_hasb(nxt) ? 2 : 1) * rowb);
+#else
+        dma_copy_at(oblk, 2 * rowb * nxt, nbuf, (pair_hasb(nxt) ? 2 : 1) * rowb);
+#endif
       }
       // this lane's env: lanes 0..31 env A, 32..63 env B (env A again when there is no B)
       const int kl = (hb && hasB) ? k0 + 1 : k0;
