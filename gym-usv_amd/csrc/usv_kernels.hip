@@ -1065,18 +1065,24 @@ __device__ __forceinline__ void lidar_window2(float dx, float dy, float key, flo
   int* const mslot = L.mark + (off & (kWave - 1));
   int carry = 0;
   QMARK(2);
-  // pair q = base + l of a pass whose max-scanned mark is mk: owner, ray, exact test, ds_min
-  auto pair = [&](int base, int mk) {
+  // pair q = base + l of a pass whose max-scanned mark is mk: owner, ray, exact test, ds_min.
+  // pair_ld reads the owner's record and the ray, pair_do tests and takes the ds_min; the two-pass
+  // case issues both passes' reads before either test (one LDS round trip for both).
+  struct PairIn { float4 o; float2 cs; int si; };
+  auto pair_ld = [&](int base, int mk) {
     const int jj = mk >> 16;                          // owner obstacle lane
     // slot of (owner env, ray) of pair q = base + l: q + (mk & 0xffff) - 32768, of which only the
     // low 8 bits are used (= those of q + mk); exact for q < W, other lanes (no hit) read some
     // ray's offsets
     const int si = base + l + mk;
-    const float4 o = rec[jj];                         // owner's (a, b, r^2, key bits)
-    const float2 cs = L.rayoff[si & 127];
+    return PairIn{rec[jj], L.rayoff[si & 127], si};   // owner's (a, b, r^2, key bits), ray (cos, sin)
+  };
+  auto pair_do = [&](int base, const PairIn& p) {
+    const float4 o = p.o;
+    const float2 cs = p.cs;
     // the key half of the payload before the hit branch (the whole record is read by one
     // ds_read_b128: the key is not re-read inside the branch)
-    unsigned long long* const sl = &L.slot[si & 255];
+    unsigned long long* const sl = &L.slot[p.si & 255];
     const unsigned kb = __float_as_uint(o.w);
     asm volatile("" :: "v"(kb));
     const float proj = fmaf(o.x, cs.x, o.y * cs.y);
@@ -1087,6 +1093,7 @@ __device__ __forceinline__ void lidar_window2(float dx, float dy, float key, flo
     if (hit)                                          // slots: env A's rays, then env B's
       atomicMin(sl, ((unsigned long long)kb << 32) | __float_as_uint(dist));
   };
+  auto pair = [&](int base, int mk) { pair_do(base, pair_ld(base, mk)); };
   int base = 0, pass = 0;
   if (W > kWave) {
     // passes 0 and 1 at once (1.65 passes per env pair on average at C3): pass 1's marks go to mark2, 64 ints
@@ -1104,8 +1111,14 @@ __device__ __forceinline__ void lidar_window2(float dx, float dy, float key, flo
     wave_incl_max2_asm(m0, m1);
     m1 = max(m1, __builtin_amdgcn_readlane(m0, 63));
     carry = __builtin_amdgcn_readlane(m1, 63);
+#ifdef USV_PAIR_SERIAL
     pair(0, m0);
     pair(kWave, m1);
+#else
+    const PairIn p0 = pair_ld(0, m0), p1 = pair_ld(kWave, m1);
+    pair_do(0, p0);
+    pair_do(kWave, p1);
+#endif
     base = 2 * kWave;
     pass = 2;
   }

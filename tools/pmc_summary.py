@@ -37,14 +37,21 @@ def all_rows(d, pattern):
     return out
 
 
-def counter(d, name, skip=5):
-    """Mean per dispatch of `name` over every counter CSV under `d` (one per --pmc pass)."""
-    vals = [float(r["Counter_Value"]) for r in all_rows(d, "*counter_collection.csv")
-            if STEP_RE.search(r["Kernel_Name"]) and r["Counter_Name"] == name]
-    if not vals:
+def counter(d, name, skip=5, regex=None):
+    """Per step: the sum over the step's kernels (names matching `regex`, default the step kernels) of
+    each kernel's mean per dispatch of `name`, over every counter CSV under `d` (one per --pmc pass)."""
+    regex = regex or STEP_RE
+    per = {}
+    for r in all_rows(d, "*counter_collection.csv"):
+        if regex.search(r["Kernel_Name"]) and r["Counter_Name"] == name:
+            per.setdefault(r["Kernel_Name"].split("(")[0], []).append(float(r["Counter_Value"]))
+    if not per:
         raise SystemExit(f"no step-kernel {name} samples under {d}")
-    vals = vals[skip:] or vals
-    return sum(vals) / len(vals), len(vals)
+    total = 0.0
+    for v in per.values():
+        v = v[skip:] or v
+        total += sum(v) / len(v)
+    return total, min(len(v) for v in per.values())
 
 
 def main():
@@ -57,17 +64,23 @@ def main():
     ap.add_argument("--out", default="profiles")
     ap.add_argument("--sq", default=None, help="directory of SQ counter passes (SQ_INSTS_VALU / SALU)")
     ap.add_argument("--envs", type=int, default=65536)
+    ap.add_argument("--kernels", default=None,
+                    help="regex of the kernels one step launches (default: the step kernels; usv-asmc-simple "
+                         "kind 6 also runs asmc_chain_kernel)")
     a = ap.parse_args()
+    rx = re.compile(a.kernels) if a.kernels else STEP_RE
     stats = [r for r in rows(a.kt, "*kernel_stats.csv") if "usv::" in r["Name"]]
-    step = [r for r in stats if STEP_RE.search(r["Name"])]
-    fetch_kib, nf = counter(a.fetch, "FETCH_SIZE")
-    write_kib, nw = counter(a.write, "WRITE_SIZE")
+    step = [r for r in stats if rx.search(r["Name"])]
+    fetch_kib, nf = counter(a.fetch, "FETCH_SIZE", regex=rx)
+    write_kib, nw = counter(a.write, "WRITE_SIZE", regex=rx)
     summ = {
         "key": a.key,
         "kernel_stats": [{k: r[k] for k in ("Name", "Calls", "AverageNs", "MinNs", "MaxNs", "Percentage")}
                          for r in stats[:8]],
         "step_kernel": step[0]["Name"] if step else None,
-        "step_kernel_avg_ns": float(step[0]["AverageNs"]) if step else None,
+        "step_kernels": [r["Name"] for r in step],
+        # every kernel of one step (their average durations summed)
+        "step_kernel_avg_ns": sum(float(r["AverageNs"]) for r in step) if step else None,
         "fetch_kib_per_launch": fetch_kib, "write_kib_per_launch": write_kib,
         "fetch_samples": nf, "write_samples": nw,
         "hbm_bytes_per_launch": round((2 * fetch_kib + write_kib) * 1024),
@@ -77,7 +90,7 @@ def main():
     if a.sq:          # wave-instruction counts per launch, for roofline.valu_frac (bench.py)
         for name in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVES"):
             try:
-                v, _ = counter(a.sq, name)
+                v, _ = counter(a.sq, name, regex=rx)
             except SystemExit:
                 continue
             summ[name.lower() + "_per_launch"] = v
