@@ -65,6 +65,7 @@ template <typename R> struct State {
   const R* exp;            // custom experiment applied by every reset, or null (kExp* layout)
   int N, cap, limit, autoreset;
   int prio;                // scan loops: raise the issue priority of lagging waves (s_setprio)
+  int rowspan;             // block-queue step: store an env pair's obs rows as one 32-B-aligned span
   int fstride;             // elements between fields (>= N, 256-B aligned)
   int ostride;             // obstacle plane stride: cap rounded up to a multiple of 4
   uint64_t seed, gid0;
@@ -134,9 +135,14 @@ template <typename T> __device__ __forceinline__ void st_obs(T* p, T v) {
   st_out(p, v);
 #endif
 }
-#ifndef USV_ROW_STORE
-#define USV_ROW_STORE 1    // 1: pair spans from 32-B sectors (round 4); 0: per-row pieces (round 3)
-#endif
+// Obs-row store layout of the block-queue step (State::rowspan; usv_set_kernel_variant lid bits 0x100 /
+// 0x200 force it on / off): an env pair's two rows as one span of 32-B-aligned 256-B stores (round 4),
+// or each row in pieces (the sensor halves, then both headers in one store).  The span writes
+// 1.05x the algorithmic bytes (pieces: 1.18x, sectors split between write-through stores) and wins
+// where the rows go to DRAM (524 288 envs: 183.4 -> 161.4 us per step); with the working set in the
+// 256 MB Infinity Cache the pieces are faster (65 536 envs: 19.2 vs 20.3 us), so the default switches
+// at kRowSpanFrom envs.
+constexpr int kRowSpanFrom = 196608;
 // Division and square root of the per-step dynamics: in the f32 build the hardware reciprocal and
 // square root (1 ulp; the reference's float64 values are matched to SURVEY 8(c)'s tolerance), which
 // shortens the dependent chain of the block queue's phase 1 (barrier exit 3.4 -> 2.6 us); IEEE in
@@ -2042,7 +2048,7 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
     const float* const rk = recs + ((hb && cB) ? c0 + 1 : c0) * kQRec;
     P = *reinterpret_cast<const float4*>(rk);
     M = *reinterpret_cast<const float4*>(rk + 4);
-    const int hl = min(max(l - ((USV_ROW_STORE && cB) ? pair_shift(c) : 0), 0), 2 * kHdr - 1);
+    const int hl = min(max(l - ((S.rowspan && cB) ? pair_shift(c) : 0), 0), 2 * kHdr - 1);
     const int hi = hl >= kHdr ? hl - kHdr : hl;
     float v = recs[((hl >= kHdr && cB) ? c0 + 1 : c0) * kQRec + (hi == 0 ? 6 : (hi <= 9 ? hi + 5 : 15))];
     // make_header's constant entries 1, 10, 13 (0) and 12, 14 (max_acceleration / 10), as selects:
@@ -2081,7 +2087,7 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
       const int nt = __float_as_int(meta.y);
       // the pair's span offset and the lane rotations of the two scans that put each reading in the
       // lane that stores it (no env B: the rows are stored as in round 3, unrotated)
-      const bool span2 = USV_ROW_STORE && hasB;
+      const bool span2 = S.rowspan && hasB;
       const int sh = span2 ? pair_shift(cur) : 0;
       const int rotA = span2 ? kHdr + sh : 0, rotB = span2 ? 2 * kHdr + sh : 0;
       Scan<float> sa, sb;
@@ -2737,6 +2743,7 @@ int carve(Handle* h, State<R>& S) {
   S.limit = h->cfg.max_episode_steps;
   S.autoreset = h->cfg.autoreset;
   S.prio = h->prio;
+  S.rowspan = h->cfg.num_envs >= kRowSpanFrom;
   S.seed = h->cfg.seed;
   S.gid0 = h->cfg.env_id_offset;
   // ray offsets start + i*res (usv_asmc_ca_env.py:420), cos/sin in float64 on the host
@@ -3230,6 +3237,10 @@ int usv_set_kernel_variant(void* hp, int32_t kind, int32_t epb, int32_t lid) {
   if (!h) return fail(USV_ERR_ARG, "null handle");
   if (is_legacy(h->cfg.mode)) return fail(USV_ERR_ARG, "the legacy ids have one lane-per-env kernel");
   const usv_config* cfg = &h->cfg;
+  // lid bits 0x100 / 0x200: the block-queue step's row-span stores forced on / off (State::rowspan)
+  const int rs = lid & 0x300;
+  lid &= 0xff;
+  if (rs == 0x300 || (rs && kind != 4 && kind != 5 && kind != 6)) return fail(USV_ERR_ARG, "bad row-store bits");
   const bool lid_ok = lid == 0 || lid == 3 || lid == 7;
   const bool wave_ok = kind == 1 && (epb == 16 || epb == 32 || epb == 64) && lid_ok;
   const bool split_ok = kind == 2 && (epb == 8 || epb == 16 || epb == 32 ||
@@ -3250,6 +3261,8 @@ int usv_set_kernel_variant(void* hp, int32_t kind, int32_t epb, int32_t lid) {
   h->epb = epb;
   h->lid = lid;
   h->prio = kind >= 4 ? 0 : 1;
+  h->sf.prio = h->sd.prio = h->prio;
+  h->sf.rowspan = h->sd.rowspan = rs ? rs == 0x100 : h->cfg.num_envs >= kRowSpanFrom;
   return USV_OK;
 }
 

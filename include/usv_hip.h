@@ -269,7 +269,9 @@ int usv_asmc_compute(int32_t precision, int32_t n, const void* act_dev, void* po
  *   kind 4 / 5: split / fused block-queue step (epb 128; kind 5 also 16), f32 window lidar, cap <= 32
  *   kind 6: usv-asmc-simple only: the ASMC chain in its own launch, then the fused block-queue step
  *           (epb 128 | 16), f32 window lidar, cap <= 32
- *   lid: lidar variant bits (0 brute, 3 brute + blind-sector skip + unroll, 7 angular window)
+ *   lid: lidar variant bits (0 brute, 3 brute + blind-sector skip + unroll, 7 angular window); kinds 4-6
+ *        also take 0x100 / 0x200: obs rows stored as 32-B-aligned env-pair spans forced on / off (default:
+ *        on from 196 608 envs, where the rows go to DRAM)
  * Waits for in-flight launches first.  USV_ERR_ARG if the handle's config cannot run it. */
 int usv_set_kernel_variant(void* handle, int32_t kind, int32_t epb, int32_t lid);
 

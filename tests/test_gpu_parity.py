@@ -341,7 +341,8 @@ def test_step_variants_bit_identical(env_id, precision):
     acts = [torch.rand(n, 2, device="cuda", generator=gen) * torch.tensor([0.8, 2.0], device="cuda")
             + torch.tensor([0.2, -1.0], device="cuda") for _ in range(T)]
     ref = None
-    queue = ("128,7,4", "128,7,5", "16,7,5") if precision == "f32" else ()   # block queue: f32 only
+    # block queue: f32 only (lid 263 / 519: obs rows as aligned env-pair spans forced on / off)
+    queue = ("128,7,4", "128,7,5", "16,7,5", "128,263,5", "16,263,5", "128,519,5") if precision == "f32" else ()
     if precision == "f32" and env_id == "usv-asmc-simple":
         queue += ("128,7,6", "16,7,6")                # ASMC chain kernel + fused block queue
     if precision == "f64":                            # f64: split scan at 16 envs/wave; block-wide dynamics
@@ -372,7 +373,7 @@ def test_block_queue_ragged_sizes(n):
     acts = [torch.rand(n, 2, device="cuda", generator=gen) * torch.tensor([0.8, 2.0], device="cuda")
             + torch.tensor([0.2, -1.0], device="cuda") for _ in range(T)]
     ref = None
-    for v in ("64,7,1", "128,7,5", "16,7,5", "128,7,4", "16,7,2"):
+    for v in ("64,7,1", "128,7,5", "16,7,5", "128,7,4", "16,7,2", "128,263,5", "16,263,5", "128,263,4"):
         env = make("usv-simple", n, seed=6, max_episode_steps=12, kernel_variant=v, copy=False)
         env.reset(seed=6)
         outs = []
@@ -405,7 +406,7 @@ def test_step_variants_bit_identical_scattered(precision):
     assert far.mean() > 0.1, far.mean()          # the far path is actually exercised
     a = torch.from_numpy(rng.uniform([0.2, -1], [1, 1], size=(n, 2)).astype(np.float32)).cuda()
     ref = None
-    queue = ("128,7,4", "128,7,5", "16,7,5") if precision == "f32" else ("64,7,2", "64,7,3", "32,7,3")
+    queue = ("128,7,4", "128,7,5", "16,7,5", "128,263,5") if precision == "f32" else ("64,7,2", "64,7,3", "32,7,3")
     for v in ("64,7,1", "32,3,1", "32,7,1", "16,0,1", "16,3,2", "8,7,2", "16,7,2") + queue:
         # copy=False: final_obs rows of envs that did not end keep the (identical) buffer contents
         env = make("usv-simple", n, seed=3, precision=precision, kernel_variant=v, copy=False)

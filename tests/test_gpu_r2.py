@@ -470,6 +470,7 @@ def test_two_process_sharding_bit_identical():
     ("usv-simple", "f32", None, 8192),        # small block-queue step (kind 5, 16 envs on 8 waves)
     ("usv-simple", "f32", None, 65536),       # the headline 128-env / 16-wave block-queue step (kind 5)
     ("usv-simple", "f32", "128,7,5", 8192),   # the same kernel forced at a small count (ragged tail too)
+    ("usv-simple", "f32", "128,263,5", 8192), # with the obs rows stored as aligned env-pair spans
     ("usv-asmc-simple", "f32", None, 8192),   # ASMC chain kernel + small block-queue step (kind 6)
     ("usv-asmc-simple", "f32", None, 65536),  # the same with 128-env blocks (the usv-asmc-simple default)
     ("usv-asmc-simple", "f32", "128,7,4", 8192),   # split block-queue step (kind 4)

@@ -55,6 +55,8 @@ def test_asmc_highspeed_replay(golden, precision, perturb):
     worst = dict(hdr=0.0, rew=0.0, vel=0.0, pos=0.0, state=0.0)
     flips = rays = 0
     cont = np.array([k for k in range(16) if k not in (11, 12)])    # continuous state entries
+    band = idx % 3                              # gen_asmc_highspeed: |psi| <= pi, <= 30, 300..400 rad
+    bw = {b: dict(hdr=0.0, rew=0.0, flips=0) for b in range(3)}
     for t in range(T):
         a = torch.from_numpy(g["actions"][idx, t]).cuda()
         obs, rew, term, trunc, info = env.step(a)
@@ -75,13 +77,21 @@ def test_asmc_highspeed_replay(golden, precision, perturb):
             worst["pos"] = max(worst["pos"], float((np.abs(ipos[m] - rp) / np.maximum(1, np.abs(rp))).max()))
             d = np.abs(st[m][:, cont] - rs[m][:, cont]) / np.maximum(1, np.abs(rs[m][:, cont]))
             worst["state"] = max(worst["state"], float(d.max()))
+            for b in range(3):
+                mb = m & (band == b)
+                if mb.any():
+                    rb = g["final_obs"][idx][mb, t]
+                    bw[b]["hdr"] = max(bw[b]["hdr"], float((np.abs(obs[mb, :15] - rb[:, :15]) - 1e-4 * np.abs(rb[:, :15])).max()))
+                    bw[b]["rew"] = max(bw[b]["rew"], float(np.abs(rew[mb] - g["reward"][idx][mb, t]).max()))
+                    bw[b]["flips"] += int((np.abs(obs[mb, 15:] - rb[:, 15:]) > 1e-5 + 1e-4 * np.abs(rb[:, 15:])).sum())
             np.testing.assert_array_equal(term[m], g["terminated"][idx][m, t], err_msg=f"t={t}")
             np.testing.assert_array_equal(trunc[m], g["truncated"][idx][m, t], err_msg=f"t={t}")
         alive &= ~(g["terminated"][idx][:, t] | g["truncated"][idx][:, t])
     fast = int(orc.asmc.fast_substeps.sum())
     print(f"\n[asmc highspeed {precision} perturb={perturb}] {fast} substeps with |u| > 1.2 over {n} envs; "
           f"Ka-switch flips {int(flipped.sum())}/{n} envs; "
-          + ", ".join(f"{k} {v:.2e}" for k, v in worst.items()) + f"; sensor flips {flips}/{rays}")
+          + ", ".join(f"{k} {v:.2e}" for k, v in worst.items()) + f"; sensor flips {flips}/{rays}; by |psi| band "
+          + "; ".join(f"{b}: hdr {v['hdr']:.2e} rew {v['rew']:.2e} flips {v['flips']}" for b, v in bw.items()))
     assert fast > 0 and (orc.asmc.fast_substeps > 0).sum() >= n // 3
     assert flipped.sum() <= (0 if precision == "f64" else max(2, n // 8)), flipped.sum()
     tol = HS_TOL[precision]
@@ -233,7 +243,7 @@ def test_asmc_split_chain_bit_identical(n):
     acts = [torch.rand(n, 2, device="cuda", generator=gen) * torch.tensor([0.8, 2.0], device="cuda")
             + torch.tensor([0.2, -1.0], device="cuda") for _ in range(T)]
     ref = None
-    for v in ("64,7,1", "128,7,4", "128,7,6", "16,7,6", None):
+    for v in ("64,7,1", "128,7,4", "128,7,6", "16,7,6", "128,263,6", None):
         env = make("usv-asmc-simple", n, seed=6, max_episode_steps=11, kernel_variant=v, copy=False, info=True)
         env.reset(seed=6)
         outs = []

@@ -28,11 +28,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--envs", type=int, default=65536)
     ap.add_argument("--warm", type=int, default=200)
+    ap.add_argument("--variant", default=None, help="kernel variant epb,lid,kind (e.g. 128,263,5: row spans on)")
     args = ap.parse_args()
     import gym_usv_amd
     lib = gym_usv_amd.load_library()
     lib.usv_diag_qprof.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
-    env = gym_usv_amd.make_vec("usv-simple", args.envs, seed=1)
+    env = gym_usv_amd.make_vec("usv-simple", args.envs, seed=1, kernel_variant=args.variant)
     env.reset(seed=1)
     g = torch.Generator(device="cuda").manual_seed(0)
     lo, span = torch.tensor([0.2, -1.0], device="cuda"), torch.tensor([0.8, 2.0], device="cuda")
