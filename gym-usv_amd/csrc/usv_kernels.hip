@@ -42,7 +42,8 @@ enum RealField {
 // Device state.  All real SoA fields share one allocation (field i at freal + i*fstride) and
 // the int fields another, so the kernel holds two base pointers instead of twenty (kernel
 // arguments live in SGPRs; fewer of them keeps the kernel at <= 80 SGPRs = 8 blocks per CU).
-enum IntField { I_NOBS, I_ELAPSED, I_EPISODE, I_SCAN, I_NINT };
+// I_TURNS (f32 usv-simple / usv-asmc-simple): whole turns of the heading, see store_heading
+enum IntField { I_NOBS, I_ELAPSED, I_EPISODE, I_SCAN, I_TURNS, I_NINT };
 template <typename R> struct State {
   R* freal;                // [F_NREAL][fstride]
   int32_t* fint;           // [I_NINT][fstride]
@@ -75,6 +76,49 @@ template <typename R> struct State {
   __host__ __device__ R* orow(int e) const { return obst + (size_t)e * 3 * ostride; }
 };
 constexpr int kV0Last = 0, kV0Aux = 9, kV0Target = 12, kV0ALast = 18, kV0Ye = 19, kV0N = 21;
+
+// Heading representation of the f32 usv-simple / usv-asmc-simple state.  The reference integrates the
+// heading without wrapping (simple_env.py:323, usv_asmc.py:234), so it grows without bound, and a float
+// of 400 rad holds it to only +-1.5e-5 rad: every step's rounding then moved the angle feature
+// (obs[3] = angle / pi) by ~5e-6 and the pose by the heading error times the distance run.  The f32
+// state keeps psi = phi + 2 pi k instead: phi (F_PSI, a float within about a turn of zero) and the
+// whole turns k (I_TURNS, int), with UsvAsmc's psi_d_last in phi's frame; the host state interface
+// returns phi + 2 pi k in float64.  Every use of the heading is through sin / cos, wrap(. - psi) or
+// differences, which are 2 pi-periodic or frame-free.  The f64 build keeps the reference's absolute
+// heading (k = 0 always) and its arithmetic order.
+constexpr float kTwoPiHi = 6.28318548f, kTwoPiLo = 1.74845553e-07f;   // 2 pi = hi - lo (float split)
+template <typename R> __device__ __forceinline__ R turns_of(R psi) { return rint(psi * R(0.15915494309189535)); }
+// psi - 2 pi n in float, the high part exact by Sterbenz for |n| <= 1 and |psi| within a turn or two
+__device__ __forceinline__ float sub_turns(float psi, float n) { return fmaf(n, kTwoPiLo, fmaf(-n, kTwoPiHi, psi)); }
+// A reset's heading (drawn, or the custom experiment's), with its whole turns split off in the f32 build
+template <typename R> __device__ __forceinline__ void store_heading(const State<R>& S, int e, R psi) {
+  if constexpr (std::is_same<R, float>::value) {
+    const float n = turns_of(psi);
+    S.F(F_PSI)[e] = sub_turns(psi, n);
+    S.I(I_TURNS)[e] = (int)n;
+  } else {
+    S.F(F_PSI)[e] = psi;
+  }
+}
+// The f32 step: once the heading phi has left [-pi, pi], move a turn into k (and the frame-bound
+// psi_d_last with it); lanes whose heading stayed in range store nothing.
+__device__ __forceinline__ void rebase_heading(const State<float>& S, int e, float& phi, float* psi_d_last) {
+  const float n = turns_of(phi);
+  if (n != 0.0f) {
+    phi = sub_turns(phi, n);
+    if (psi_d_last) *psi_d_last = sub_turns(*psi_d_last, n);
+    S.I(I_TURNS)[e] += (int)n;
+  }
+}
+// phi + 2 pi k of env e (the reference's heading) in R: for the info row
+template <typename R> __device__ __forceinline__ R heading_abs(const State<R>& S, int e, R phi) {
+  if constexpr (std::is_same<R, float>::value) {
+    const float k = (float)S.I(I_TURNS)[e];
+    return fmaf(-k, kTwoPiLo, fmaf(k, kTwoPiHi, phi));
+  } else {
+    return phi;
+  }
+}
 // custom experiment record (usv_experiment, simple_env.py:292-300), in R: n, path start (2),
 // path angle, pose (3), pad, then x[cap], y[cap], r[cap]
 constexpr int kExpN = 0, kExpPS = 1, kExpAngle = 3, kExpPose = 4, kExpObs = 8;
@@ -262,7 +306,8 @@ __device__ __forceinline__ void reset_experiment(const State<R>& S, int e, int e
   m_sincos(X[kExpAngle], &sx2, &cx2);
   const R pe0 = ps0 + cx2 * R(100), pe1 = ps1 + sx2 * R(100);                     // :296
   const R px = X[kExpPose], py = X[kExpPose + 1], psi = X[kExpPose + 2];
-  S.F(F_X)[e] = px; S.F(F_Y)[e] = py; S.F(F_PSI)[e] = psi;
+  S.F(F_X)[e] = px; S.F(F_Y)[e] = py;
+  store_heading<R>(S, e, psi);
   S.F(F_PX0)[e] = ps0; S.F(F_PY0)[e] = ps1;
   S.F(F_PX1)[e] = pe0; S.F(F_PY1)[e] = pe1;
   S.I(I_NOBS)[e] = cnt;
@@ -341,7 +386,8 @@ __device__ __forceinline__ void reset_wave(const State<R>& S, int e, float* row,
     const R refv = R(0.75) + (mu - R(0.75)) * bcast(U.u[0], 35);
     R sa, ca;
     m_sincos(ang, &sa, &ca);
-    S.F(F_X)[e] = sx; S.F(F_Y)[e] = sy; S.F(F_PSI)[e] = psi;
+    S.F(F_X)[e] = sx; S.F(F_Y)[e] = sy;
+    store_heading<R>(S, e, psi);
     S.F(F_U)[e] = u; S.F(F_V)[e] = v; S.F(F_R)[e] = r;
     S.F(F_PROGRESS)[e] = R(0);
     S.F(F_PX0)[e] = sx; S.F(F_PY0)[e] = sy;
@@ -366,6 +412,7 @@ __device__ __forceinline__ void reset_wave(const State<R>& S, int e, float* row,
 // sin/cos of the heading used by the lidar; the step kernel and the reset kernel (stale scan)
 // must use this same function so their scans are bit-identical
 template <typename R> __device__ __forceinline__ void heading_sincos(R psi, R* s, R* c) { fx_sincos(psi, s, c); }
+
 
 // --------------------------------------------------------------------------- NumPy-exact reset
 // numpy.random.Generator(PCG64) as the reference's reset uses it (simple_env.py:234-290), one lane
@@ -503,7 +550,8 @@ __device__ void np_reset(const State<R>& S, int e, float* row, R* info = nullptr
   if (MODE == USV_MODE_ASMC_SIMPLE)
     for (int i = 0; i < kAsmcN; ++i) S.asmc[(size_t)i * S.N + e] = R(0);
   const R x0 = R(px), y0 = R(py), ps = R(pp);
-  S.F(F_X)[e] = x0; S.F(F_Y)[e] = y0; S.F(F_PSI)[e] = ps;
+  S.F(F_X)[e] = x0; S.F(F_Y)[e] = y0;
+  store_heading<R>(S, e, ps);
   S.F(F_U)[e] = R(u); S.F(F_V)[e] = R(v); S.F(F_R)[e] = R(r);
   S.F(F_PROGRESS)[e] = R(0);
   S.F(F_PX0)[e] = R(ps0); S.F(F_PY0)[e] = R(ps1);
@@ -603,6 +651,7 @@ __device__ __forceinline__ void asmc_env_chain(const State<R>& S, int e, int el0
         for (int k = 0; k < 20; ++k) asmc_substep_f32(s, c0, c1, x, y, psi, u, v, r, xl, yl, pl, kt, 0, false);
       }
       x += xl; y += yl; psi += pl;
+      rebase_heading(S, e, psi, &s[0]);              // psi_d_last moves with the heading's frame
     } else {
       if (pert) {
         for (int k = 0; k < 20; ++k) asmc_substep<R>(s, c0, c1, x, y, psi, u, v, r, 20 * el0 + k, true);
@@ -678,19 +727,21 @@ __device__ void env_dynamics(const State<R>& S, int e, float a_u, float a_r, flo
   const R dact_r = -(dact / R(2)) * R(0.15);
   partial = ye_r + ang_r + vel_r + dact_r;
   if (info) {                                        // _get_info + reward_info (:102-115, :189-199)
-    const R vals[USV_INFO_DIM] = {x, y, psi, u, v, r, x0, y0, S.F(F_PX1)[e], S.F(F_PY1)[e], a3u, a3r, ye,
+    const R vals[USV_INFO_DIM] = {x, y, heading_abs(S, e, psi), u, v, r, x0, y0, S.F(F_PX1)[e], S.F(F_PY1)[e], a3u, a3r, ye,
                                   cdiv(angle, kPi), ye_r, ang_r, dact_r, dact, vel_r, refv, lu, lu - refv};
 #pragma unroll
     for (int i = 0; i < USV_INFO_DIM; ++i) info[i] = vals[i];
   }
+  px = x; py = y;
+  heading_sincos(psi, &psp, &pcp);
+  // usv-simple: the step's heading, rebased (usv-asmc-simple rebases in its ASMC chain, with psi_d_last)
+  if constexpr (std::is_same<R, float>::value && MODE == USV_MODE_SIMPLE) rebase_heading(S, e, psi, nullptr);
   S.F(F_X)[e] = x; S.F(F_Y)[e] = y; S.F(F_PSI)[e] = psi;
   S.F(F_U)[e] = u; S.F(F_V)[e] = v; S.F(F_R)[e] = r;
   S.F(F_LAST_U)[e] = a3u; S.F(F_LAST_R)[e] = a3r;
   S.F(F_PROGRESS)[e] = a;
   S.I(I_ELAPSED)[e] = el;
   S.I(I_SCAN)[e] = 1;
-  px = x; py = y;
-  heading_sincos(psi, &psp, &pcp);
 }
 
 // --------------------------------------------------------------------------- lidar
@@ -2957,9 +3008,57 @@ int field_io(Handle* h, State<R>& S, int f, void* host, bool to_host) {
   if (rc == USV_OK && !to_host) HIP_TRY(hipDeviceSynchronize());
   return rc;
 }
+// f32 usv-simple / usv-asmc-simple keep the heading as phi + 2 pi k (store_heading): the host sees
+// and sets the reference's heading, and UsvAsmc's psi_d_last in the reference's frame.
+template <typename R>
+bool turn_frame(const Handle* h) {
+  return std::is_same<R, float>::value && !is_legacy(h->cfg.mode);
+}
+template <typename R>
+int heading_io(Handle* h, State<R>& S, int f, double* hd, bool to_host) {
+  const size_t N = (size_t)S.N;
+  constexpr double kTwoPi = 2.0 * kPi;
+  std::vector<int32_t> k(N);
+  HIP_TRY(hipMemcpy(k.data(), S.I(I_TURNS), N * 4, hipMemcpyDeviceToHost));
+  std::vector<R> t(N);
+  R* dev = f == USV_FIELD_PSI ? S.F(F_PSI) : S.asmc;          // ASMC row 0: psi_d_last
+  if (to_host) {
+    HIP_TRY(hipMemcpy(t.data(), dev, N * sizeof(R), hipMemcpyDeviceToHost));
+    for (size_t e = 0; e < N; ++e) {
+      const double v = (double)t[e] + kTwoPi * k[e];
+      if (f == USV_FIELD_PSI) hd[e] = v;
+      else hd[e * kAsmcN] = v;
+    }
+    return USV_OK;
+  }
+  if (f == USV_FIELD_ASMC) {
+    HIP_TRY(hipMemcpy(t.data(), dev, N * sizeof(R), hipMemcpyDeviceToHost));   // (rows 1.. already written)
+    for (size_t e = 0; e < N; ++e) t[e] = (R)(hd[e * kAsmcN] - kTwoPi * k[e]);
+    HIP_TRY(hipMemcpy(dev, t.data(), N * sizeof(R), hipMemcpyHostToDevice));
+    return USV_OK;
+  }
+  // a new heading: new whole turns, and usv-asmc-simple's psi_d_last moved into the new frame
+  std::vector<int32_t> kn(N);
+  for (size_t e = 0; e < N; ++e) {
+    const double n = std::nearbyint(hd[e] / kTwoPi);
+    kn[e] = (int32_t)n;
+    t[e] = (R)(hd[e] - kTwoPi * n);
+  }
+  HIP_TRY(hipMemcpy(dev, t.data(), N * sizeof(R), hipMemcpyHostToDevice));
+  if (h->cfg.mode == USV_MODE_ASMC_SIMPLE) {
+    std::vector<R> s0(N);
+    HIP_TRY(hipMemcpy(s0.data(), S.asmc, N * sizeof(R), hipMemcpyDeviceToHost));
+    for (size_t e = 0; e < N; ++e) s0[e] = (R)((double)s0[e] + kTwoPi * (k[e] - kn[e]));
+    HIP_TRY(hipMemcpy(S.asmc, s0.data(), N * sizeof(R), hipMemcpyHostToDevice));
+  }
+  HIP_TRY(hipMemcpy(S.I(I_TURNS), kn.data(), N * 4, hipMemcpyHostToDevice));
+  return USV_OK;
+}
+
 template <typename R>
 int field_io_impl(Handle* h, State<R>& S, int f, void* host, bool to_host) {
   const size_t N = (size_t)S.N;
+  if (f == USV_FIELD_PSI && turn_frame<R>(h)) return heading_io<R>(h, S, f, (double*)host, to_host);
   if (f < F_NREAL) {
     std::vector<R> tmp(N);
     double* hd = (double*)host;
@@ -3024,6 +3123,8 @@ int field_io_impl(Handle* h, State<R>& S, int f, void* host, bool to_host) {
         for (int i = 0; i < kAsmcN; ++i) tmp[(size_t)i * N + e] = (R)hd[e * kAsmcN + i];
       HIP_TRY(hipMemcpy(S.asmc, tmp.data(), cnt * sizeof(R), hipMemcpyHostToDevice));
     }
+    // psi_d_last between the reference's frame (host) and the heading's (device, f32)
+    if (turn_frame<R>(h)) return heading_io<R>(h, S, f, hd, to_host);
     return USV_OK;
   }
   if (f == USV_FIELD_NP_RNG || f == USV_FIELD_NP_MT) {   // device SoA uint32 rows, host [N][per] int32
