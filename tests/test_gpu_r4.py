@@ -258,3 +258,52 @@ def test_asmc_split_chain_bit_identical(n):
         for t, (a_, b_) in enumerate(zip(ref, outs)):
             for x, y in zip(a_, b_):
                 assert torch.equal(x, y), f"variant {v} differs at step {t} (n={n})"
+
+
+@pytest.mark.parametrize("env_id", ["usv-simple", "usv-asmc-simple"])
+def test_f32_heading_turns_roundtrip_and_spin(env_id):
+    """The f32 state holds the heading as phi + 2 pi k: a heading of ~400 rad set through the state
+    interface reads back to float precision of phi (not float32's 3e-5 at 400 rad), psi_d_last
+    keeps its value across a frame change (usv-asmc-simple), and a usv-simple rollout spinning at
+    full yaw (the heading passing tens of turns) keeps the f32 obs header within 2e-5 of the f64
+    kernel's."""
+    n = 64
+    envs = {p: make(env_id, n, precision=p, autoreset=False, reset_rng="numpy", max_episode_steps=0)
+            for p in ("f32", "f64")}
+    for e in envs.values():
+        e.reset(seed=list(range(900, 900 + n)))
+    e32 = envs["f32"]
+    psi = np.linspace(-400.3, 400.7, n)
+    e32.set_field("psi", psi)
+    assert np.abs(e32.get_field("psi") - psi).max() < 1e-6
+    if env_id == "usv-asmc-simple":
+        st = e32.get_field("asmc")
+        st[:, 0] = psi + 0.25
+        e32.set_field("asmc", st)
+        e32.set_field("psi", psi + 12.0)                 # a new frame: psi_d_last keeps its value
+        assert np.abs(e32.get_field("asmc")[:, 0] - (psi + 0.25)).max() < 1e-5
+        e32.set_field("psi", psi)
+        e32.set_field("asmc", np.zeros((n, 16)))
+    if env_id != "usv-simple":          # (the ASMC's switching law makes f32 and f64 rollouts part ways)
+        for e in envs.values():
+            e.close()
+        return
+    envs["f64"].set_state(e32.get_state())
+    a = torch.tensor([[0.3, 1.0]] * n, device="cuda")
+    alive = np.ones(n, bool)
+    worst = 0.0
+    for t in range(300):
+        o32, _, te, tr, _ = e32.step(a)
+        o64, _, te64, tr64, _ = envs["f64"].step(a)
+        o32, o64, te, tr, te64, tr64 = to_np(o32, o64, te, tr, te64, tr64)
+        alive &= ~(te | tr | te64 | tr64)
+        if not alive.any():
+            break
+        worst = max(worst, float(np.abs(o32[alive, :15] - o64[alive, :15]).max()))
+    spin = np.abs(e32.get_field("psi") - psi).max()
+    print(f"\n[{env_id} heading turns] |psi| up to {np.abs(e32.get_field('psi')).max():.1f} rad "
+          f"(moved {spin:.1f} rad), f32 vs f64 obs header max err {worst:.2e}, {int(alive.sum())} envs alive")
+    assert alive.sum() >= n // 4 and spin > 20
+    assert worst <= 2e-5, worst
+    for e in envs.values():
+        e.close()
