@@ -100,14 +100,16 @@ template <typename R> __device__ __forceinline__ void store_heading(const State<
     S.F(F_PSI)[e] = psi;
   }
 }
-// The f32 step: once the heading phi has left [-pi, pi], move a turn into k (and the frame-bound
-// psi_d_last with it); lanes whose heading stayed in range store nothing.
-__device__ __forceinline__ void rebase_heading(const State<float>& S, int e, float& phi, float* psi_d_last) {
+// End of an f32 step: once the heading phi has left [-pi, pi], move its whole turns into k, and
+// (usv-asmc-simple) UsvAsmc's psi_d_last with it; lanes whose heading stayed in range store nothing.
+// The stored phi is therefore always within [-pi, pi], so the host's phi + 2 pi k splits back into
+// the same (phi, k).
+__device__ __forceinline__ void rebase_heading(const State<float>& S, int e, float& phi, bool asmc) {
   const float n = turns_of(phi);
   if (n != 0.0f) {
     phi = sub_turns(phi, n);
-    if (psi_d_last) *psi_d_last = sub_turns(*psi_d_last, n);
     S.I(I_TURNS)[e] += (int)n;
+    if (asmc) S.asmc[e] = sub_turns(S.asmc[e], n);   // row 0: psi_d_last
   }
 }
 // phi + 2 pi k of env e (the reference's heading) in R: for the info row
@@ -651,7 +653,6 @@ __device__ __forceinline__ void asmc_env_chain(const State<R>& S, int e, int el0
         for (int k = 0; k < 20; ++k) asmc_substep_f32(s, c0, c1, x, y, psi, u, v, r, xl, yl, pl, kt, 0, false);
       }
       x += xl; y += yl; psi += pl;
-      rebase_heading(S, e, psi, &s[0]);              // psi_d_last moves with the heading's frame
     } else {
       if (pert) {
         for (int k = 0; k < 20; ++k) asmc_substep<R>(s, c0, c1, x, y, psi, u, v, r, 20 * el0 + k, true);
@@ -734,8 +735,7 @@ __device__ void env_dynamics(const State<R>& S, int e, float a_u, float a_r, flo
   }
   px = x; py = y;
   heading_sincos(psi, &psp, &pcp);
-  // usv-simple: the step's heading, rebased (usv-asmc-simple rebases in its ASMC chain, with psi_d_last)
-  if constexpr (std::is_same<R, float>::value && MODE == USV_MODE_SIMPLE) rebase_heading(S, e, psi, nullptr);
+  if constexpr (std::is_same<R, float>::value) rebase_heading(S, e, psi, MODE == USV_MODE_ASMC_SIMPLE);
   S.F(F_X)[e] = x; S.F(F_Y)[e] = y; S.F(F_PSI)[e] = psi;
   S.F(F_U)[e] = u; S.F(F_V)[e] = v; S.F(F_R)[e] = r;
   S.F(F_LAST_U)[e] = a3u; S.F(F_LAST_R)[e] = a3r;
