@@ -104,19 +104,26 @@ template <typename R> __device__ __forceinline__ void store_heading(const State<
 // (usv-asmc-simple) UsvAsmc's psi_d_last with it; lanes whose heading stayed in range store nothing.
 // The stored phi is therefore always within [-pi, pi], so the host's phi + 2 pi k splits back into
 // the same (phi, k).
-__device__ __forceinline__ void rebase_heading(const State<float>& S, int e, float& phi, bool asmc) {
-  const float n = turns_of(phi);
-  if (n != 0.0f) {
-    phi = sub_turns(phi, n);
-    S.I(I_TURNS)[e] += (int)n;
-    if (asmc) S.asmc[e] = sub_turns(S.asmc[e], n);   // row 0: psi_d_last
+// k and psi_d_last move by atomic adds that return nothing: no load, so nothing in the step waits on them
+// (a read-modify-write here made phase 1 wait for every store of the dynamics before it).
+template <typename R>
+__device__ __forceinline__ void rebase_heading(const State<R>& S, int e, R& phi, bool asmc) {
+  if constexpr (std::is_same<R, float>::value) {
+    const float n = turns_of(phi);
+    if (n != 0.0f) {
+      phi = sub_turns(phi, n);
+      __hip_atomic_fetch_add(S.I(I_TURNS) + e, (int)n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (asmc)                                      // row 0: psi_d_last -= 2 pi n
+        __hip_atomic_fetch_add(S.asmc + e, fmaf(n, kTwoPiLo, -n * kTwoPiHi), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
-// phi + 2 pi k of env e (the reference's heading) in R: for the info row
-template <typename R> __device__ __forceinline__ R heading_abs(const State<R>& S, int e, R phi) {
+// phi + 2 pi k (the reference's heading) in R: for the info row
+template <typename R> __device__ __forceinline__ R heading_abs(R phi, int k) {
   if constexpr (std::is_same<R, float>::value) {
-    const float k = (float)S.I(I_TURNS)[e];
-    return fmaf(-k, kTwoPiLo, fmaf(k, kTwoPiHi, phi));
+    const float kf = (float)k;
+    return fmaf(-kf, kTwoPiLo, fmaf(kf, kTwoPiHi, phi));
   } else {
     return phi;
   }
@@ -631,7 +638,7 @@ __global__ __launch_bounds__(kBlock) void asmc_compute_kernel(int n, const R* __
 // e's pose and velocity, in registers; the ASMC state is loaded and stored here.
 template <typename R>
 __device__ __forceinline__ void asmc_env_chain(const State<R>& S, int e, int el0, float a_u, float a_r, R& x,
-                                               R& y, R& psi, R& u, R& v, R& r) {
+                                               R& y, R& psi, R& u, R& v, R& r, R* psi_d_last = nullptr) {
   {
     R s[kAsmcN];
 #pragma unroll
@@ -663,6 +670,7 @@ __device__ __forceinline__ void asmc_env_chain(const State<R>& S, int e, int el0
     }
 #pragma unroll
     for (int i = 0; i < kAsmcN; ++i) S.asmc[(size_t)i * S.N + e] = s[i];
+    if (psi_d_last) *psi_d_last = s[0];
   }
 }
 
@@ -728,14 +736,15 @@ __device__ void env_dynamics(const State<R>& S, int e, float a_u, float a_r, flo
   const R dact_r = -(dact / R(2)) * R(0.15);
   partial = ye_r + ang_r + vel_r + dact_r;
   if (info) {                                        // _get_info + reward_info (:102-115, :189-199)
-    const R vals[USV_INFO_DIM] = {x, y, heading_abs(S, e, psi), u, v, r, x0, y0, S.F(F_PX1)[e], S.F(F_PY1)[e], a3u, a3r, ye,
+    const R vals[USV_INFO_DIM] = {x, y, heading_abs(psi, std::is_same<R, float>::value ? S.I(I_TURNS)[e] : 0), u, v, r,
+                                  x0, y0, S.F(F_PX1)[e], S.F(F_PY1)[e], a3u, a3r, ye,
                                   cdiv(angle, kPi), ye_r, ang_r, dact_r, dact, vel_r, refv, lu, lu - refv};
 #pragma unroll
     for (int i = 0; i < USV_INFO_DIM; ++i) info[i] = vals[i];
   }
   px = x; py = y;
   heading_sincos(psi, &psp, &pcp);
-  if constexpr (std::is_same<R, float>::value) rebase_heading(S, e, psi, MODE == USV_MODE_ASMC_SIMPLE);
+  rebase_heading<R>(S, e, psi, MODE == USV_MODE_ASMC_SIMPLE);
   S.F(F_X)[e] = x; S.F(F_Y)[e] = y; S.F(F_PSI)[e] = psi;
   S.F(F_U)[e] = u; S.F(F_V)[e] = v; S.F(F_R)[e] = r;
   S.F(F_LAST_U)[e] = a3u; S.F(F_LAST_R)[e] = a3r;
@@ -1706,13 +1715,13 @@ __device__ __forceinline__ void step_body_wave(const State<R>& S, const IO<R>& i
   if (ne > 0) {
     const int e = e0 + min(l, ne - 1);
     const float2 a = reinterpret_cast<const float2*>(io.act)[e];
+    nl = S.I(I_NOBS)[e];                              // (ahead of the dynamics' stores)
     float hdr[kHdr];
     env_dynamics<R, MODE>(S, e, a.x, a.y, hdr, px, py, sp, cp, partial, trunc,
                              io.info ? io.info + (size_t)e * USV_INFO_DIM : nullptr);
     float* row = io.obs + (size_t)e * kObsDim;
 #pragma unroll
     for (int i = 0; i < kHdr; ++i) row[i] = hdr[i];   // lane-per-env rows: plain stores (L2 merges them)
-    nl = S.I(I_NOBS)[e];
   }
   const unsigned trunc_m = (unsigned)ballot(trunc);
   USV_STAMP_W(1);
@@ -1748,6 +1757,7 @@ __global__ __launch_bounds__(kBlock) void dyn_kernel(State<R> S, IO<R> io) {
   const int e = blockIdx.x * kBlock + threadIdx.x;
   if (e >= S.N) return;
   const float2 a = reinterpret_cast<const float2*>(io.act)[e];
+  const int nob = S.I(I_NOBS)[e];                    // (ahead of the dynamics' stores)
   float hdr[kHdr];
   R px, py, sp, cp, partial;
   bool trunc;
@@ -1757,7 +1767,7 @@ __global__ __launch_bounds__(kBlock) void dyn_kernel(State<R> S, IO<R> io) {
 #pragma unroll
   for (int i = 0; i < kHdr; ++i) row[i] = hdr[i];     // lane-per-env rows: plain stores (L2 merges them)
   S.pose[2 * (size_t)e] = R4<R>{px, py, sp, cp};
-  S.pose[2 * (size_t)e + 1] = R4<R>{partial, R(S.I(I_NOBS)[e]), R(trunc ? 1 : 0), R(0)};
+  S.pose[2 * (size_t)e + 1] = R4<R>{partial, R(nob), R(trunc ? 1 : 0), R(0)};
   io.rew[e] = partial;
   io.trunc[e] = trunc;
 }
@@ -1844,6 +1854,7 @@ __device__ __forceinline__ void step_body_blockdyn(const State<R>& S, const IO<R
     // divergent memory operations: hipcc's vmcnt bookkeeping stays exact around the DMAs)
     const int e = eb + min(l, nbe - 1);
     const float2 a = reinterpret_cast<const float2*>(io.act)[e];
+    const int nob = S.I(I_NOBS)[e];                        // (ahead of the dynamics' stores)
     float hdr[kHdr];
     R px, py, sp, cp, partial;
     bool trunc;
@@ -1853,7 +1864,7 @@ __device__ __forceinline__ void step_body_blockdyn(const State<R>& S, const IO<R
 #pragma unroll
     for (int i = 0; i < kHdr; ++i) row[i] = hdr[i];         // lane-per-env rows: plain stores
     rec[l] = R4<R>{px, py, sp, cp};
-    rec[kWave + l] = R4<R>{partial, R(S.I(I_NOBS)[e]), R(trunc ? 1 : 0), R(0)};
+    rec[kWave + l] = R4<R>{partial, R(nob), R(trunc ? 1 : 0), R(0)};
     USV_STAMP_W(1);
     if (io.fobs) {
       // waves 1-3 read these header rows back for their done envs' terminal obs (emit_env): every
@@ -1996,7 +2007,7 @@ __device__ __forceinline__ void q_emit_done(const State<float>& S, const IO<floa
 constexpr int kQE_S = USV_QE_S, kQW_S = 8;
 constexpr int kQSmallBelow = 32768;   // env count below which the small blocks are the default (tools/nsweep.sh)
 template <int QE = kQE, int QW = kQW> __host__ __device__ constexpr size_t lds_q_bytes() {
-  return wave_tab_bytes<float>() + QW * q_slice_bytes() + QE * kQRec * 4 + 16;
+  return wave_tab_bytes<float>() + QW * q_slice_bytes() + QE * kQRec * 4 + 16 + QE * 4;   // + n_obs[QE]
 }
 static_assert(2 * lds_q_bytes() <= 160 * 1024, "two blocks per CU");
 static_assert(4 * lds_q_bytes<kQE_S, kQW_S>() <= 160 * 1024, "four small blocks per CU");
@@ -2005,7 +2016,11 @@ static_assert(4 * lds_q_bytes<kQE_S, kQW_S>() <= 160 * 1024, "four small blocks 
 // the raw step (usv_step, io.done null) then carries neither the pointer nor its branch in the pair
 // loop, whose SGPR budget is at its limit (a runtime test cost 0.25 us per launch).
 // CHAIN = false (usv-asmc-simple, FUSED): asmc_chain_kernel ran the ASMC chain, phase 1 the rest.
-template <int MODE, bool FUSED, bool DONE = false, int kQE = ::usv::kQE, int kQW = ::usv::kQW, bool CHAIN = true>
+// INFO (fused): phase 1 writes the per-step info rows (usv_step_ex with info_dev); a template switch
+// like DONE: the info path's registers would otherwise make phase 1 spill, and the spill's reload
+// wait for every store the dynamics issued before the barrier.
+template <int MODE, bool FUSED, bool DONE = false, int kQE = ::usv::kQE, int kQW = ::usv::kQW, bool CHAIN = true,
+          bool INFO = false>
 __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<float>& io) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
@@ -2021,6 +2036,7 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
   float* const rowbuf1 = rowbuf0 + 256;
   float* const recs = reinterpret_cast<float*>(lds + wave_tab_bytes<float>() + kQW * q_slice_bytes());
   unsigned* const qctr = reinterpret_cast<unsigned*>(recs + kQE * kQRec);
+  int* const qnob = reinterpret_cast<int*>(recs + kQE * kQRec) + 4;   // fused: the block's n_obs
   const float2* const rayoff = reinterpret_cast<const float2*>(lds);
 #ifdef USV_DIAG_QPROF
   QProf qprof;
@@ -2029,7 +2045,8 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
   QProf* const qp = nullptr;
 #endif
   if (threadIdx.x == 0) *qctr = kQW;                   // pairs 0 .. kQW-1 are the static first ones
-  if (wave == 0) dma_copy(S.ray_tab, lds, (int)wave_tab_bytes<float>());
+  // the ray table: by the last wave, so that the dynamics waves (fused) issue no DMA of their own
+  if (wave == kQW - 1) dma_copy(S.ray_tab, lds, (int)wave_tab_bytes<float>());
 #pragma unroll
   for (int i = 0; i < 4; ++i) slot[i * 64 + l] = kSlotArm;
   mark[l] = 0;                                         // lidar_window2 clears them after each call
@@ -2040,7 +2057,7 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
   // also issue those of waves 0 and 1, whose state loads would otherwise queue behind their own DMA
   // (a wave's loads return in issue order); the barrier below publishes them.
   constexpr int kDynWaves = FUSED ? (kQE + kWave - 1) / kWave : 0;
-  static_assert(kQW >= 2 * kDynWaves && 2 * kQW <= kQE + 2 * kWave, "block shape");
+  static_assert(kQW >= 3 * kDynWaves + 1 && 2 * kQW <= kQE + 2 * kWave, "block shape");
   if (wave >= kDynWaves && cur >= 0) dma_copy1(S.orow(eb + 2 * cur), rowbuf0, min(2, nbe - 2 * cur) * rowb);
   if (FUSED && wave >= kDynWaves && wave < 2 * kDynWaves) {
     const int w = wave - kDynWaves;
@@ -2049,6 +2066,13 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
                 min(2, nbe - 2 * w) * rowb);
   }
   if constexpr (FUSED) {
+    // the block's obstacle counts into LDS by waves 2 kDynWaves .. 3 kDynWaves - 1 (one env per lane),
+    // so the dynamics waves load nothing after their stores: a load issued after them would make the
+    // wave wait for every store's ack (one vmcnt counter) before the barrier
+    if (wave >= 2 * kDynWaves && wave < 3 * kDynWaves) {
+      const int k = (wave - 2 * kDynWaves) * kWave + l;
+      if (k < nbe) qnob[k] = S.I(I_NOBS)[eb + k];
+    }
     // dynamics, one lane per env.  Lanes past the end repeat the wave's last env (same wave:
     // every lane loads the state before any lane stores it); a wave with no env of its own must
     // not run, or two waves would race on the same env's state
@@ -2060,17 +2084,18 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
       float px, py, sp, cp, partial;
       bool trunc;
       env_dynamics<float, MODE, CHAIN>(S, e, a.x, a.y, hdr, px, py, sp, cp, partial, trunc,
-                                       io.info ? io.info + (size_t)e * USV_INFO_DIM : nullptr);
+                                       INFO ? io.info + (size_t)e * USV_INFO_DIM : nullptr);
       io.trunc[e] = trunc;
-      make_qrec(recs + k * kQRec, px, py, sp, cp, partial, S.I(I_NOBS)[e], trunc, hdr);
+      make_qrec(recs + k * kQRec, px, py, sp, cp, partial, 0, trunc, hdr);   // (n_obs: qnob)
     }
   } else {
     if (wave < kQE / 16 && wave * 16 < nbe)            // 16 records (1 KiB) per wave
       dma_copy1(S.qrec + (size_t)(eb + wave * 16) * kQRec, recs + wave * 16 * kQRec, min(16, nbe - wave * 16) * kQRec * 4);
   }
-  // rows, ray table and records landed
+  // rows, ray table and records landed (the dynamics waves issued no DMA: their stores drain later,
+  // ahead of their first pair's rows in the vmcnt order)
   USV_STAMP_W(1);
-  vm_wait<0>();
+  if (wave >= kDynWaves) vm_wait<0>();
   QMARK(10);
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   USV_STAMP_W(2);
@@ -2096,9 +2121,11 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
   auto rec_of = [&](int c, float4& P, float4& M, float& H) {
     const int c0 = 2 * c;
     const bool cB = pair_hasb(c);
-    const float* const rk = recs + ((hb && cB) ? c0 + 1 : c0) * kQRec;
+    const int kk = (hb && cB) ? c0 + 1 : c0;
+    const float* const rk = recs + kk * kQRec;
     P = *reinterpret_cast<const float4*>(rk);
     M = *reinterpret_cast<const float4*>(rk + 4);
+    if constexpr (FUSED) M.y = __int_as_float(__float_as_int(M.y) | qnob[kk]);   // n_obs | truncated << 16
     const int hl = min(max(l - ((S.rowspan && cB) ? pair_shift(c) : 0), 0), 2 * kHdr - 1);
     const int hi = hl >= kHdr ? hl - kHdr : hl;
     float v = recs[((hl >= kHdr && cB) ? c0 + 1 : c0) * kQRec + (hi == 0 ? 6 : (hi <= 9 ? hi + 5 : 15))];
@@ -2222,12 +2249,12 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
   USV_STAMP_W(6);
 }
 
-template <int MODE, bool FUSED, bool DONE, bool CHAIN = true>
+template <int MODE, bool FUSED, bool DONE, bool CHAIN = true, bool INFO = false>
 __global__ __launch_bounds__(kQW * kWave) __attribute__((amdgpu_num_sgpr(USV_QSGPR), amdgpu_waves_per_eu(USV_QWPE, USV_QWPE)))
-void step_q_kernel(State<float> S, IO<float> io) { step_q_body<MODE, FUSED, DONE, kQE, kQW, CHAIN>(S, io); }
-template <int MODE, bool DONE, bool CHAIN = true>
+void step_q_kernel(State<float> S, IO<float> io) { step_q_body<MODE, FUSED, DONE, kQE, kQW, CHAIN, INFO>(S, io); }
+template <int MODE, bool DONE, bool CHAIN = true, bool INFO = false>
 __global__ __launch_bounds__(kQW_S * kWave) __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8)))
-void step_qs_kernel(State<float> S, IO<float> io) { step_q_body<MODE, true, DONE, kQE_S, kQW_S, CHAIN>(S, io); }
+void step_qs_kernel(State<float> S, IO<float> io) { step_q_body<MODE, true, DONE, kQE_S, kQW_S, CHAIN, INFO>(S, io); }
 
 // Split block-queue step, first half: full-width lane-per-env dynamics writing the env records
 // (make_qrec) for step_q_kernel<MODE, false, DONE>, plus truncated and the info row.
@@ -2236,13 +2263,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 2))) 
   const int e = blockIdx.x * kBlock + threadIdx.x;
   if (e >= S.N) return;
   const float2 a = reinterpret_cast<const float2*>(io.act)[e];
+  const int nob = S.I(I_NOBS)[e];                  // (ahead of the dynamics' stores)
   float hdr[kHdr];
   float px, py, sp, cp, partial;
   bool trunc;
   env_dynamics<float, MODE>(S, e, a.x, a.y, hdr, px, py, sp, cp, partial, trunc,
                             io.info ? io.info + (size_t)e * USV_INFO_DIM : nullptr);
   io.trunc[e] = trunc;
-  make_qrec(S.qrec + (size_t)e * kQRec, px, py, sp, cp, partial, S.I(I_NOBS)[e], trunc, hdr);
+  make_qrec(S.qrec + (size_t)e * kQRec, px, py, sp, cp, partial, nob, trunc, hdr);
 }
 
 // usv-asmc-simple, split at the ASMC chain (kind 6): the two UsvAsmc.compute calls of every env,
@@ -2858,20 +2886,24 @@ void* pick_scan(int epw, int lid) {
   return pick_scan_lid<R, MODE, 4, WPB>(lid);
 }
 
-// split_chain (kind 6, usv-asmc-simple): the fused q kernel without the ASMC chain in its phase 1
-template <bool DONE>
+// split_chain (kind 6, usv-asmc-simple): the fused q kernel without the ASMC chain in its phase 1;
+// info: the fused kernels' info-row instantiation (the split kind 4 writes info in dyn_rec_kernel)
+template <bool DONE, bool INFO>
 void* pick_q_done(int mode, bool fused, bool small, bool split_chain) {
   const bool simple = mode == USV_MODE_SIMPLE;
   if (!simple && split_chain)
-    return small ? (void*)&step_qs_kernel<USV_MODE_ASMC_SIMPLE, DONE, false>
-                 : (void*)&step_q_kernel<USV_MODE_ASMC_SIMPLE, true, DONE, false>;
-  if (small) return simple ? (void*)&step_qs_kernel<USV_MODE_SIMPLE, DONE> : (void*)&step_qs_kernel<USV_MODE_ASMC_SIMPLE, DONE>;
-  if (fused) return simple ? (void*)&step_q_kernel<USV_MODE_SIMPLE, true, DONE>
-                           : (void*)&step_q_kernel<USV_MODE_ASMC_SIMPLE, true, DONE>;
+    return small ? (void*)&step_qs_kernel<USV_MODE_ASMC_SIMPLE, DONE, false, INFO>
+                 : (void*)&step_q_kernel<USV_MODE_ASMC_SIMPLE, true, DONE, false, INFO>;
+  if (small) return simple ? (void*)&step_qs_kernel<USV_MODE_SIMPLE, DONE, true, INFO>
+                           : (void*)&step_qs_kernel<USV_MODE_ASMC_SIMPLE, DONE, true, INFO>;
+  if (fused) return simple ? (void*)&step_q_kernel<USV_MODE_SIMPLE, true, DONE, true, INFO>
+                           : (void*)&step_q_kernel<USV_MODE_ASMC_SIMPLE, true, DONE, true, INFO>;
   return simple ? (void*)&step_q_kernel<USV_MODE_SIMPLE, false, DONE> : (void*)&step_q_kernel<USV_MODE_ASMC_SIMPLE, false, DONE>;
 }
-void* pick_q(int mode, bool fused, bool small = false, bool done = false, bool split_chain = false) {
-  return done ? pick_q_done<true>(mode, fused, small, split_chain) : pick_q_done<false>(mode, fused, small, split_chain);
+void* pick_q(int mode, bool fused, bool small = false, bool done = false, bool split_chain = false, bool info = false) {
+  if (info && fused)
+    return done ? pick_q_done<true, true>(mode, fused, small, split_chain) : pick_q_done<false, true>(mode, fused, small, split_chain);
+  return done ? pick_q_done<true, false>(mode, fused, small, split_chain) : pick_q_done<false, false>(mode, fused, small, split_chain);
 }
 
 template <typename R>
@@ -2928,7 +2960,8 @@ int launch_step_kernels(Handle* h, State<R>& S, const float* act, float* obs, vo
         HIP_TRY(hipLaunchKernel((void*)&asmc_chain_kernel<float>, dim3((S.N + kBlock - 1) / kBlock), dim3(kBlock), args, 0, st));
       const bool small = h->kind != 4 && h->epb == kQE_S;
       const int qe = small ? kQE_S : kQE, qw = small ? kQW_S : kQW;
-      HIP_TRY(hipLaunchKernel(pick_q(h->cfg.mode, h->kind != 4, small, io.done != nullptr, h->kind == 6),
+      HIP_TRY(hipLaunchKernel(pick_q(h->cfg.mode, h->kind != 4, small, io.done != nullptr, h->kind == 6,
+                                     io.info != nullptr),
                               dim3((S.N + qe - 1) / qe), dim3(qw * kWave), args,
                               small ? lds_q_bytes<kQE_S, kQW_S>() : lds_q_bytes(), st));
       return USV_OK;
@@ -3193,13 +3226,14 @@ int set_experiment(Handle* h, State<R>& S, const usv_experiment* x) {
 int queue_lds_attr(const Handle* h) {
   if (h->kind != 4 && h->kind != 5 && h->kind != 6) return USV_OK;
   const bool split = h->kind == 6;
-  for (const bool done : {false, true}) {
-    HIP_TRY(hipFuncSetAttribute(pick_q(h->cfg.mode, h->kind != 4, false, done, split),
-                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_q_bytes()));
-    if (h->kind != 4)
-      HIP_TRY(hipFuncSetAttribute(pick_q(h->cfg.mode, true, true, done, split), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)lds_q_bytes<kQE_S, kQW_S>()));
-  }
+  for (const bool done : {false, true})
+    for (const bool info : {false, true}) {
+      HIP_TRY(hipFuncSetAttribute(pick_q(h->cfg.mode, h->kind != 4, false, done, split, info),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_q_bytes()));
+      if (h->kind != 4)
+        HIP_TRY(hipFuncSetAttribute(pick_q(h->cfg.mode, true, true, done, split, info),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_q_bytes<kQE_S, kQW_S>()));
+    }
   return USV_OK;
 }
 
