@@ -100,25 +100,13 @@ template <typename R> __device__ __forceinline__ void store_heading(const State<
     S.F(F_PSI)[e] = psi;
   }
 }
-// End of an f32 step: once the heading phi has left [-pi, pi], move its whole turns into k, and
-// (usv-asmc-simple) UsvAsmc's psi_d_last with it; lanes whose heading stayed in range store nothing.
-// The stored phi is therefore always within [-pi, pi], so the host's phi + 2 pi k splits back into
-// the same (phi, k).
-// k and psi_d_last move by atomic adds that return nothing: no load, so nothing in the step waits on them
-// (a read-modify-write here made phase 1 wait for every store of the dynamics before it).
-template <typename R>
-__device__ __forceinline__ void rebase_heading(const State<R>& S, int e, R& phi, bool asmc) {
-  if constexpr (std::is_same<R, float>::value) {
-    const float n = turns_of(phi);
-    if (n != 0.0f) {
-      phi = sub_turns(phi, n);
-      __hip_atomic_fetch_add(S.I(I_TURNS) + e, (int)n, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (asmc)                                      // row 0: psi_d_last -= 2 pi n
-        __hip_atomic_fetch_add(S.asmc + e, fmaf(n, kTwoPiLo, -n * kTwoPiHi), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
+// End of an f32 step (env_dynamics): once the heading phi has left [-pi, pi], its whole turns move
+// into k, and (usv-asmc-simple) UsvAsmc's psi_d_last with it, so the stored phi is always within
+// [-pi, pi] and the host's phi + 2 pi k splits back into the same (phi, k).  k and psi_d_last are
+// loaded with the rest of the state and stored back plain: a load after the dynamics' stores would
+// make the wave wait for their acks (one vmcnt counter), and atomic adds are wrong for the lanes that
+// repeat a wave's last env (each would add the turns again), where plain stores of the same value
+// are not.
 // phi + 2 pi k (the reference's heading) in R: for the info row
 template <typename R> __device__ __forceinline__ R heading_abs(R phi, int k) {
   if constexpr (std::is_same<R, float>::value) {
@@ -639,6 +627,7 @@ __global__ __launch_bounds__(kBlock) void asmc_compute_kernel(int n, const R* __
 template <typename R>
 __device__ __forceinline__ void asmc_env_chain(const State<R>& S, int e, int el0, float a_u, float a_r, R& x,
                                                R& y, R& psi, R& u, R& v, R& r, R* psi_d_last = nullptr) {
+  // psi_d_last given: row 0 (psi_d_last) is returned there and not stored (the caller rebases it)
   {
     R s[kAsmcN];
 #pragma unroll
@@ -669,7 +658,7 @@ __device__ __forceinline__ void asmc_env_chain(const State<R>& S, int e, int el0
       }
     }
 #pragma unroll
-    for (int i = 0; i < kAsmcN; ++i) S.asmc[(size_t)i * S.N + e] = s[i];
+    for (int i = psi_d_last ? 1 : 0; i < kAsmcN; ++i) S.asmc[(size_t)i * S.N + e] = s[i];
     if (psi_d_last) *psi_d_last = s[0];
   }
 }
@@ -685,8 +674,16 @@ __device__ void env_dynamics(const State<R>& S, int e, float a_u, float a_r, flo
   R x = S.F(F_X)[e], y = S.F(F_Y)[e], psi = S.F(F_PSI)[e];
   R u = S.F(F_U)[e], v = S.F(F_V)[e], r = S.F(F_R)[e];
   const int el0 = S.I(I_ELAPSED)[e];
-  if (MODE == USV_MODE_ASMC_SIMPLE) {
-    if constexpr (CHAIN) asmc_env_chain<R>(S, e, el0, a_u, a_r, x, y, psi, u, v, r);
+  constexpr bool kF32 = std::is_same<R, float>::value;
+  constexpr bool kAsmc = MODE == USV_MODE_ASMC_SIMPLE;
+  int k0 = 0;                                        // f32: the heading's whole turns (store_heading)
+  R pdl = R(0);                                      // f32 usv-asmc-simple: psi_d_last, phi's frame
+  if constexpr (kF32) {
+    k0 = S.I(I_TURNS)[e];
+    if constexpr (kAsmc && !CHAIN) pdl = S.asmc[e];
+  }
+  if (kAsmc) {
+    if constexpr (CHAIN) asmc_env_chain<R>(S, e, el0, a_u, a_r, x, y, psi, u, v, r, kF32 ? &pdl : nullptr);
     a_u = 0.0f;                                                                   // step(zeros(2))
     a_r = 0.0f;
   }
@@ -736,7 +733,7 @@ __device__ void env_dynamics(const State<R>& S, int e, float a_u, float a_r, flo
   const R dact_r = -(dact / R(2)) * R(0.15);
   partial = ye_r + ang_r + vel_r + dact_r;
   if (info) {                                        // _get_info + reward_info (:102-115, :189-199)
-    const R vals[USV_INFO_DIM] = {x, y, heading_abs(psi, std::is_same<R, float>::value ? S.I(I_TURNS)[e] : 0), u, v, r,
+    const R vals[USV_INFO_DIM] = {x, y, heading_abs(psi, k0), u, v, r,
                                   x0, y0, S.F(F_PX1)[e], S.F(F_PY1)[e], a3u, a3r, ye,
                                   cdiv(angle, kPi), ye_r, ang_r, dact_r, dact, vel_r, refv, lu, lu - refv};
 #pragma unroll
@@ -744,7 +741,17 @@ __device__ void env_dynamics(const State<R>& S, int e, float a_u, float a_r, flo
   }
   px = x; py = y;
   heading_sincos(psi, &psp, &pcp);
-  rebase_heading<R>(S, e, psi, MODE == USV_MODE_ASMC_SIMPLE);
+  if constexpr (kF32) {                              // the rebase (see the heading representation)
+    const float n = turns_of(psi);
+    if (n != 0.0f) {
+      psi = sub_turns(psi, n);
+      S.I(I_TURNS)[e] = k0 + (int)n;
+      if constexpr (kAsmc) pdl = sub_turns(pdl, n);
+    }
+    if constexpr (kAsmc) {
+      if (CHAIN || n != 0.0f) S.asmc[e] = pdl;       // (the chain left row 0 to this store)
+    }
+  }
   S.F(F_X)[e] = x; S.F(F_Y)[e] = y; S.F(F_PSI)[e] = psi;
   S.F(F_U)[e] = u; S.F(F_V)[e] = v; S.F(F_R)[e] = r;
   S.F(F_LAST_U)[e] = a3u; S.F(F_LAST_R)[e] = a3r;
