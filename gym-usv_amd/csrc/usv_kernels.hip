@@ -177,7 +177,8 @@ template <typename T> __device__ __forceinline__ void st_obs(T* p, T v) {
 #endif
 }
 // Obs-row store layout of the block-queue step (State::rowspan; usv_set_kernel_variant lid bits 0x100 /
-// 0x200 force it on / off): an env pair's two rows as one span of 32-B-aligned 256-B stores (round 4),
+// 0x200 force it on / off; a template switch, SPAN, of the 128-env fused kernels without info rows, as
+// the two layouts' code together in the pair loop spilled SGPRs; the others store pieces): an env pair's two rows as one span of 32-B-aligned 256-B stores (round 4),
 // or each row in pieces (the sensor halves, then both headers in one store).  The span writes
 // 1.05x the algorithmic bytes (pieces: 1.18x, sectors split between write-through stores) and wins
 // where the rows go to DRAM (524 288 envs: 183.4 -> 161.4 us per step); with the working set in the
@@ -2027,7 +2028,7 @@ static_assert(4 * lds_q_bytes<kQE_S, kQW_S>() <= 160 * 1024, "four small blocks 
 // like DONE: the info path's registers would otherwise make phase 1 spill, and the spill's reload
 // wait for every store the dynamics issued before the barrier.
 template <int MODE, bool FUSED, bool DONE = false, int kQE = ::usv::kQE, int kQW = ::usv::kQW, bool CHAIN = true,
-          bool INFO = false>
+          bool INFO = false, bool SPAN = false>
 __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<float>& io) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
@@ -2133,7 +2134,7 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
     P = *reinterpret_cast<const float4*>(rk);
     M = *reinterpret_cast<const float4*>(rk + 4);
     if constexpr (FUSED) M.y = __int_as_float(__float_as_int(M.y) | qnob[kk]);   // n_obs | truncated << 16
-    const int hl = min(max(l - ((S.rowspan && cB) ? pair_shift(c) : 0), 0), 2 * kHdr - 1);
+    const int hl = min(max(l - ((SPAN && cB) ? pair_shift(c) : 0), 0), 2 * kHdr - 1);
     const int hi = hl >= kHdr ? hl - kHdr : hl;
     float v = recs[((hl >= kHdr && cB) ? c0 + 1 : c0) * kQRec + (hi == 0 ? 6 : (hi <= 9 ? hi + 5 : 15))];
     // make_header's constant entries 1, 10, 13 (0) and 12, 14 (max_acceleration / 10), as selects:
@@ -2172,7 +2173,7 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
       const int nt = __float_as_int(meta.y);
       // the pair's span offset and the lane rotations of the two scans that put each reading in the
       // lane that stores it (no env B: the rows are stored as in round 3, unrotated)
-      const bool span2 = S.rowspan && hasB;
+      const bool span2 = SPAN && hasB;
       const int sh = span2 ? pair_shift(cur) : 0;
       const int rotA = span2 ? kHdr + sh : 0, rotB = span2 ? 2 * kHdr + sh : 0;
       Scan<float> sa, sb;
@@ -2256,9 +2257,9 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
   USV_STAMP_W(6);
 }
 
-template <int MODE, bool FUSED, bool DONE, bool CHAIN = true, bool INFO = false>
+template <int MODE, bool FUSED, bool DONE, bool CHAIN = true, bool INFO = false, bool SPAN = false>
 __global__ __launch_bounds__(kQW * kWave) __attribute__((amdgpu_num_sgpr(USV_QSGPR), amdgpu_waves_per_eu(USV_QWPE, USV_QWPE)))
-void step_q_kernel(State<float> S, IO<float> io) { step_q_body<MODE, FUSED, DONE, kQE, kQW, CHAIN, INFO>(S, io); }
+void step_q_kernel(State<float> S, IO<float> io) { step_q_body<MODE, FUSED, DONE, kQE, kQW, CHAIN, INFO, SPAN>(S, io); }
 template <int MODE, bool DONE, bool CHAIN = true, bool INFO = false>
 __global__ __launch_bounds__(kQW_S * kWave) __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8)))
 void step_qs_kernel(State<float> S, IO<float> io) { step_q_body<MODE, true, DONE, kQE_S, kQW_S, CHAIN, INFO>(S, io); }
@@ -2896,8 +2897,14 @@ void* pick_scan(int epw, int lid) {
 // split_chain (kind 6, usv-asmc-simple): the fused q kernel without the ASMC chain in its phase 1;
 // info: the fused kernels' info-row instantiation (the split kind 4 writes info in dyn_rec_kernel)
 template <bool DONE, bool INFO>
-void* pick_q_done(int mode, bool fused, bool small, bool split_chain) {
+void* pick_q_done(int mode, bool fused, bool small, bool split_chain, bool span) {
   const bool simple = mode == USV_MODE_SIMPLE;
+  if constexpr (!INFO)
+    if (span && fused && !small) {                     // row-span stores (State::rowspan)
+      if (simple) return (void*)&step_q_kernel<USV_MODE_SIMPLE, true, DONE, true, false, true>;
+      return split_chain ? (void*)&step_q_kernel<USV_MODE_ASMC_SIMPLE, true, DONE, false, false, true>
+                         : (void*)&step_q_kernel<USV_MODE_ASMC_SIMPLE, true, DONE, true, false, true>;
+    }
   if (!simple && split_chain)
     return small ? (void*)&step_qs_kernel<USV_MODE_ASMC_SIMPLE, DONE, false, INFO>
                  : (void*)&step_q_kernel<USV_MODE_ASMC_SIMPLE, true, DONE, false, INFO>;
@@ -2907,10 +2914,13 @@ void* pick_q_done(int mode, bool fused, bool small, bool split_chain) {
                            : (void*)&step_q_kernel<USV_MODE_ASMC_SIMPLE, true, DONE, true, INFO>;
   return simple ? (void*)&step_q_kernel<USV_MODE_SIMPLE, false, DONE> : (void*)&step_q_kernel<USV_MODE_ASMC_SIMPLE, false, DONE>;
 }
-void* pick_q(int mode, bool fused, bool small = false, bool done = false, bool split_chain = false, bool info = false) {
+void* pick_q(int mode, bool fused, bool small = false, bool done = false, bool split_chain = false, bool info = false,
+             bool span = false) {
   if (info && fused)
-    return done ? pick_q_done<true, true>(mode, fused, small, split_chain) : pick_q_done<false, true>(mode, fused, small, split_chain);
-  return done ? pick_q_done<true, false>(mode, fused, small, split_chain) : pick_q_done<false, false>(mode, fused, small, split_chain);
+    return done ? pick_q_done<true, true>(mode, fused, small, split_chain, span)
+                : pick_q_done<false, true>(mode, fused, small, split_chain, span);
+  return done ? pick_q_done<true, false>(mode, fused, small, split_chain, span)
+              : pick_q_done<false, false>(mode, fused, small, split_chain, span);
 }
 
 template <typename R>
@@ -2968,7 +2978,7 @@ int launch_step_kernels(Handle* h, State<R>& S, const float* act, float* obs, vo
       const bool small = h->kind != 4 && h->epb == kQE_S;
       const int qe = small ? kQE_S : kQE, qw = small ? kQW_S : kQW;
       HIP_TRY(hipLaunchKernel(pick_q(h->cfg.mode, h->kind != 4, small, io.done != nullptr, h->kind == 6,
-                                     io.info != nullptr),
+                                     io.info != nullptr, S.rowspan != 0),
                               dim3((S.N + qe - 1) / qe), dim3(qw * kWave), args,
                               small ? lds_q_bytes<kQE_S, kQW_S>() : lds_q_bytes(), st));
       return USV_OK;
@@ -3235,8 +3245,9 @@ int queue_lds_attr(const Handle* h) {
   const bool split = h->kind == 6;
   for (const bool done : {false, true})
     for (const bool info : {false, true}) {
-      HIP_TRY(hipFuncSetAttribute(pick_q(h->cfg.mode, h->kind != 4, false, done, split, info),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_q_bytes()));
+      for (const bool span : {false, true})
+        HIP_TRY(hipFuncSetAttribute(pick_q(h->cfg.mode, h->kind != 4, false, done, split, info, span),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_q_bytes()));
       if (h->kind != 4)
         HIP_TRY(hipFuncSetAttribute(pick_q(h->cfg.mode, true, true, done, split, info),
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_q_bytes<kQE_S, kQW_S>()));
