@@ -680,7 +680,9 @@ __device__ void env_dynamics(const State<R>& S, int e, float a_u, float a_r, flo
   int k0 = 0;                                        // f32: the heading's whole turns (store_heading)
   R pdl = R(0);                                      // f32 usv-asmc-simple: psi_d_last, phi's frame
   if constexpr (kF32) {
+#ifndef USV_AB_NO_REBASE
     k0 = S.I(I_TURNS)[e];
+#endif
     if constexpr (kAsmc && !CHAIN) pdl = S.asmc[e];
   }
   if (kAsmc) {
@@ -742,16 +744,18 @@ __device__ void env_dynamics(const State<R>& S, int e, float a_u, float a_r, flo
   }
   px = x; py = y;
   heading_sincos(psi, &psp, &pcp);
+#ifdef USV_AB_NO_REBASE
+  if constexpr (false) {                             // (A/B timing builds only: wrong for spinning envs)
+#else
   if constexpr (kF32) {                              // the rebase (see the heading representation)
+#endif
+    // branch-free and stored unconditionally (n = 0 leaves both values unchanged, bit for bit): a
+    // conditional store made the compiler sink the k0 load into its branch, and a wave with one
+    // rebasing lane then waited a memory round trip in the middle of phase 1
     const float n = turns_of(psi);
-    if (n != 0.0f) {
-      psi = sub_turns(psi, n);
-      S.I(I_TURNS)[e] = k0 + (int)n;
-      if constexpr (kAsmc) pdl = sub_turns(pdl, n);
-    }
-    if constexpr (kAsmc) {
-      if (CHAIN || n != 0.0f) S.asmc[e] = pdl;       // (the chain left row 0 to this store)
-    }
+    psi = sub_turns(psi, n);
+    S.I(I_TURNS)[e] = k0 + (int)n;
+    if constexpr (kAsmc) S.asmc[e] = sub_turns(pdl, n);   // (the chain left row 0 to this store)
   }
   S.F(F_X)[e] = x; S.F(F_Y)[e] = y; S.F(F_PSI)[e] = psi;
   S.F(F_U)[e] = u; S.F(F_V)[e] = v; S.F(F_R)[e] = r;
@@ -2054,7 +2058,11 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
 #endif
   if (threadIdx.x == 0) *qctr = kQW;                   // pairs 0 .. kQW-1 are the static first ones
   // the ray table: by the last wave, so that the dynamics waves (fused) issue no DMA of their own
+#ifdef USV_P1_R3
+  if (wave == 0) dma_copy(S.ray_tab, lds, (int)wave_tab_bytes<float>());   // (A/B builds: round 3's phase 1)
+#else
   if (wave == kQW - 1) dma_copy(S.ray_tab, lds, (int)wave_tab_bytes<float>());
+#endif
 #pragma unroll
   for (int i = 0; i < 4; ++i) slot[i * 64 + l] = kSlotArm;
   mark[l] = 0;                                         // lidar_window2 clears them after each call
@@ -2079,7 +2087,9 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
     // wave wait for every store's ack (one vmcnt counter) before the barrier
     if (wave >= 2 * kDynWaves && wave < 3 * kDynWaves) {
       const int k = (wave - 2 * kDynWaves) * kWave + l;
+#ifndef USV_AB_NOB_LATE
       if (k < nbe) qnob[k] = S.I(I_NOBS)[eb + k];
+#endif
     }
     // dynamics, one lane per env.  Lanes past the end repeat the wave's last env (same wave:
     // every lane loads the state before any lane stores it); a wave with no env of its own must
@@ -2094,7 +2104,11 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
       env_dynamics<float, MODE, CHAIN>(S, e, a.x, a.y, hdr, px, py, sp, cp, partial, trunc,
                                        INFO ? io.info + (size_t)e * USV_INFO_DIM : nullptr);
       io.trunc[e] = trunc;
+#ifdef USV_AB_NOB_LATE
+      make_qrec(recs + k * kQRec, px, py, sp, cp, partial, S.I(I_NOBS)[e], trunc, hdr);
+#else
       make_qrec(recs + k * kQRec, px, py, sp, cp, partial, 0, trunc, hdr);   // (n_obs: qnob)
+#endif
     }
   } else {
     if (wave < kQE / 16 && wave * 16 < nbe)            // 16 records (1 KiB) per wave
@@ -2103,7 +2117,11 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
   // rows, ray table and records landed (the dynamics waves issued no DMA: their stores drain later,
   // ahead of their first pair's rows in the vmcnt order)
   USV_STAMP_W(1);
+#ifdef USV_P1_R3
+  vm_wait<0>();
+#else
   if (wave >= kDynWaves) vm_wait<0>();
+#endif
   QMARK(10);
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   USV_STAMP_W(2);
@@ -2122,6 +2140,16 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
   // instructions, 1.18x the algorithmic write bytes).  sh = the span's dword offset in its sector.
   const unsigned ob = (unsigned)(((uintptr_t)io.obs >> 2) & 7);
   auto pair_shift = [&](int p) { return (int)((ob + (unsigned)(eb + 2 * p) * (unsigned)kObsDim) & 7u); };
+  // per-row layout (SPAN = false): the obs-header lanes are loop-invariant, packed in one register:
+  // lanes 0..14 store env A's header value hi, 15..29 env B's, 30..63 repeat lane 29; the record slot
+  // of value hi (qrec_hdr) in bits 8..12, bit 16: env B's lane, bit 17: a constant entry (1, 10, 12-14)
+  int hpk = 0;
+  if constexpr (!SPAN) {
+    const int hl = min(l, 2 * kHdr - 1);
+    const int hi = hl >= kHdr ? hl - kHdr : hl;
+    const int hrec = hi == 0 ? 6 : (hi <= 9 ? hi + 5 : 15);
+    hpk = hi | (hrec << 8) | ((hl >= kHdr) << 16) | ((hi == 1 || hi == 10 || hi >= 12) << 17);
+  }
   // env record of pair c for this lane (lanes 0..31 env A, 32..63 env B; env A again when there is
   // no B): pose, meta and the obs-header value this lane stores (lanes sh..sh+14: env A's entries
   // 0..14, sh+15..sh+29: env B's; no env B: sh = 0 and lanes 15..29 repeat env A's).  Read one pair
@@ -2133,7 +2161,13 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
     const float* const rk = recs + kk * kQRec;
     P = *reinterpret_cast<const float4*>(rk);
     M = *reinterpret_cast<const float4*>(rk + 4);
+#ifndef USV_AB_NOB_LATE
     if constexpr (FUSED) M.y = __int_as_float(__float_as_int(M.y) | qnob[kk]);   // n_obs | truncated << 16
+#endif
+    if constexpr (!SPAN) {                             // (the constant entries are selected at the store)
+      H = recs[((((hpk >> 16) & 1) && cB) ? c0 + 1 : c0) * kQRec + ((hpk >> 8) & 31)];
+      return;
+    }
     const int hl = min(max(l - ((SPAN && cB) ? pair_shift(c) : 0), 0), 2 * kHdr - 1);
     const int hi = hl >= kHdr ? hl - kHdr : hl;
     float v = recs[((hl >= kHdr && cB) ? c0 + 1 : c0) * kQRec + (hi == 0 ? 6 : (hi <= 9 ? hi + 5 : 15))];
@@ -2210,8 +2244,15 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
         st_obs(rowA + kHdr + 64 + l, l_norm(sa.rd1));
         st_obs(rowB + kHdr + l, l_norm(hasB ? sb.rd0 : sa.rd0));
         st_obs(rowB + kHdr + 64 + l, l_norm(hasB ? sb.rd1 : sa.rd1));
-        const int hl = min(l, 2 * kHdr - 1);           // lanes 0..14 env A, 15..29 env B (or A again)
-        st_obs((hl >= kHdr ? rowB - kHdr : rowA) + hl, hv);
+        if constexpr (SPAN) {
+          const int hl = min(l, 2 * kHdr - 1);         // lanes 0..14 env A, 15..29 env B (or A again)
+          st_obs((hl >= kHdr ? rowB - kHdr : rowA) + hl, hv);
+        } else {
+          const int hi = hpk & 31;
+          const bool hB = ((hpk >> 16) & 1) && hasB;    // (no env B: env A's value again)
+          const float hc = hi == 12 ? (float)(kMaxAccU / 10.0) : hi == 14 ? (float)(kMaxAccR / 10.0) : 0.0f;
+          st_obs(rowA + (hB ? kObsDim : 0) + hi, ((hpk >> 17) & 1) ? hc : hv);
+        }
       }
       const bool term_l = hb ? termB : sa.term;         // reward, terminated: lanes 0..31 env A,
       const bool coll_l = hb ? collB : collA;           // 32..63 env B

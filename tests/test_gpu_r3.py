@@ -238,7 +238,8 @@ def test_asmc_simple_step_info_matches_reference(golden, precision):
     # f64: the reference's float64 arithmetic order (ASMC bit-exact); f32: 20 float32 ASMC substeps
     # per step accumulate position rounding (ye_reward's slope is 1/0.075 per metre): the trajectory
     # bound of the usv-asmc-simple golden replay (test_gpu_parity.py)
-    tol = 1e-9 if precision == "f64" else 5e-4
+    # ~5x the round-4 measurement: f64 6.2e-16 (position), f32 3.2e-5 (ye_reward)
+    tol = 5e-15 if precision == "f64" else 1.5e-4
     for k, v in worst.items():
         assert v <= tol, (k, v)
     env.close()

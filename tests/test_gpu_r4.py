@@ -31,9 +31,13 @@ def to_np(*ts):
     return [t.detach().cpu().numpy() for t in ts]
 
 
-# f32 bounds, ~5x the measured worst case (printed); f64 bounds: the reference's arithmetic
-HS_TOL = {"f64": dict(hdr=2e-6, rew=1e-8, vel=1e-9, state=1e-9),
-          "f32": dict(hdr=1e-5, rew=1e-4, vel=5e-4, state=5e-3)}
+# Bounds ~5x the worst case measured on the round-4 tree (printed by the test; profiles/r04_gpu_errors.txt),
+# capped by SURVEY 8(c) where that is tighter.  f64 measured: obs header exact, reward 3.6e-15, pose /
+# velocity 2.5e-16, ASMC state 1.8e-13 (OCML's exp / asin / sin / cos against glibc's differ in the last
+# bit, and 20 substeps carry it); f32: header 7.1e-6 (8(c) 1e-5), reward 3.5e-5 (8(c) 1e-4), pose /
+# velocity 3.5e-5 relative, state 1.6e-3.
+HS_TOL = {"f64": dict(hdr=0.0, rew=2e-14, vel=2e-15, state=1e-12),
+          "f32": dict(hdr=1e-5, rew=1e-4, vel=1.5e-4, state=5e-3)}
 
 
 @pytest.mark.parametrize("precision", ["f64", "f32"])
@@ -132,7 +136,8 @@ def test_reference_asmc_tests_on_hip(golden, precision):
         worst = max(worst, float(err.max()))
         print(f"\n[KAT {name} {precision}] final pos {position}, vel {velocity}; ref final {ref[-1]}; "
               f"first 300 calls max rel err {err.max():.2e}")
-    assert worst <= (1e-9 if precision == "f64" else 5e-4), worst
+    # measured: f64 5.7e-15, f32 4.4e-5 (kat_rot)
+    assert worst <= (3e-14 if precision == "f64" else 2.5e-4), worst
 
 
 @pytest.mark.parametrize("precision", ["f64", "f32"])
@@ -151,7 +156,8 @@ def test_asmc_compute_injected_states(golden, precision):
     e = dict(pos=rel(p, g["pos_out"]), vel=rel(v, g["vel_out"]), state=rel(st.T, ref_st))
     print(f"\n[asmc compute 192 {precision}] " + ", ".join(f"{k} {x:.2e}" for k, x in e.items())
           + f"; |u| > 1.2 inputs: {int((np.abs(g['vel_in'][:, 0]) > 1.2).sum())}")
-    tol = 1e-10 if precision == "f64" else dict(pos=2e-6, vel=5e-5, state=5e-4)
+    # measured: f64 pos 1.5e-16, vel 6.3e-16, state 7.3e-14; f32 pos 9.8e-8, vel 2.5e-7, state 5.1e-5
+    tol = 5e-13 if precision == "f64" else dict(pos=5e-7, vel=1.5e-6, state=2.5e-4)
     for k, x in e.items():
         assert x <= (tol if precision == "f64" else tol[k]), (k, x)
 
@@ -174,7 +180,7 @@ def test_asmc_compute_perturbed_sequences(golden, precision):
     (ps,) = to_np(b.perturb_step)
     print(f"\n[asmc perturb seq {precision}] 40 calls, max rel err {worst:.2e}")
     assert np.all(ps == 400)
-    assert worst <= (1e-9 if precision == "f64" else 5e-4), worst
+    assert worst <= (2e-15 if precision == "f64" else 5e-6), worst     # measured 3.4e-16 / 9.6e-7
 
 
 def test_asmc_compute_matches_env_step_f64():
