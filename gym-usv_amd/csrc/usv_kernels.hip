@@ -2187,8 +2187,9 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
     while (cur >= 0) {
       int nxt = (int)__builtin_amdgcn_readlane(tk, 0);
       QCOUNT(8, 1);
-      float* const cbuf = (it & 1) ? rowbuf1 : rowbuf0;
-      float* const nbuf = (it & 1) ? rowbuf0 : rowbuf1;
+      const bool odd = (it & 1) != 0;
+      float* const cbuf = odd ? rowbuf1 : rowbuf0;
+      float* const nbuf = odd ? rowbuf0 : rowbuf1;
       const int k0 = 2 * cur;
       const int e0 = eb + k0;
       const bool hasB = pair_hasb(cur);
