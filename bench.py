@@ -15,8 +15,10 @@ Warm-up: the W warm-up steps, then more untimed steps until --clock-warmup secon
 otherwise time a cold chip).  The line reports both counts.
 
 Rank 0 prints one JSON line: value = all ranks' env-steps / max-rank time, plus
-  roofline:     algorithmic bytes per launch / mean launch duration (HIP events around groups of
-                back-to-back launches on the env's stream) vs 8 TB/s; traffic from the committed
+  roofline:     algorithmic bytes per launch / mean launch duration (HIP events on the env's stream
+                at both ends of the K timed launches; --event-layout mid: around launches 2..K-1 in
+                groups, the round-3 layout, whose timing markers between launches cost wall time)
+                vs 8 TB/s; traffic from the committed
                 rocprofv3 PMC summary (profiles/pmc_summary.json) when it matches the workload;
                 valu_frac = VALU wave-instructions per launch (same summary, SQ_INSTS_VALU) x 2
                 cycles (a wave64 VALU instruction on a SIMD-32) / (1024 SIMDs x 2.4 GHz x launch time).
@@ -197,7 +199,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--cpu-procs", type=int, default=0, help="0 = every usable host core")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--event-every", type=int, default=16, help="launches per HIP-event-timed group")
+    ap.add_argument("--event-every", type=int, default=16, help="launches per HIP-event-timed group (mid layout)")
+    ap.add_argument("--event-layout", default="edge", choices=["edge", "mid"],
+                    help="edge: one event pair around all K timed launches; mid: groups inside the loop")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_summary.json"))
     ap.add_argument("--clock-warmup", type=float, default=0.3,
                     help="untimed steps after --warmup until this many seconds have passed")
@@ -270,27 +274,42 @@ def main():
     # per group; a pair around every single launch would add its own gap to each launch)
     # groups start after the first launch, so nothing but that launch sits between t0 and the GPU
     G = max(1, args.event_every)
-    groups = (K - 1) // G
+    edge = args.event_layout == "edge"
+    groups = 1 if edge else (K - 1) // G
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(groups)]
+    for a, b in ev:                                   # the events exist before the timed region
+        a.record(stream)
+        b.record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    launch(W2)
-    for k in range(1, K):
-        g, r = divmod(k - 1, G)
-        if g < groups and r == 0:
-            ev[g][0].record(stream)
-        launch(W2 + k)
-        if g < groups and r == G - 1:
-            ev[g][1].record(stream)
+    if edge:
+        # one timing marker before the first launch and one after the last: a marker between two
+        # launches makes the second wait for the first's end-of-kernel release (tools/probe_wall.py)
+        ev[0][0].record(stream)
+        for k in range(K):
+            launch(W2 + k)
+        ev[0][1].record(stream)
+    else:
+        launch(W2)
+        for k in range(1, K):
+            g, r = divmod(k - 1, G)
+            if g < groups and r == 0:
+                ev[g][0].record(stream)
+            launch(W2 + k)
+            if g < groups and r == G - 1:
+                ev[g][1].record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    kern_ms = (sum(a.elapsed_time(b) for a, b in ev) / (groups * G)) if groups else elapsed / K * 1e3
+    if edge:
+        kern_ms = ev[0][0].elapsed_time(ev[0][1]) / K
+    else:
+        kern_ms = (sum(a.elapsed_time(b) for a, b in ev) / (groups * G)) if groups else elapsed / K * 1e3
     elapsed, kern_ms = reduce_max([elapsed, kern_ms], device=dev)
 
     # public API leg (untimed by the contract above): UsvVectorEnv.step on the same envs
@@ -344,6 +363,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "kernel_ms": round(kern_ms, 5),
+                         "kernel_timing": ("HIP events around all K timed launches / K" if edge else
+                                           f"HIP events around {groups} group(s) of {G} launches"),
                          "algorithmic_bytes_per_env_step": round(bpe, 1),
                          "valu_frac": valu_frac,
                          "valu_basis": "SQ_INSTS_VALU per launch (profiles/pmc_summary.json) x 2 cycles / "

@@ -76,6 +76,27 @@ def main():
                 ev.append(e0.elapsed_time(e1) * 1e-3)
             out[f"wall_{K}_{how}_sync_us"] = med(xs)
             out[f"event_{K}_{how}_sync_us"] = med(ev)
+    # bench.py's round-3/4 layout: events after the first launch and after launch 17 (markers between kernels)
+    for how in ("mid_events", "edge_events", "no_events"):
+        xs = []
+        for _ in range(args.reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize(dev)
+            t = time.perf_counter()
+            if how == "edge_events":
+                e0.record(stream)
+            step(*args_)
+            for k in range(1, 20):
+                if how == "mid_events" and k == 1:
+                    e0.record(stream)
+                step(*args_)
+                if how == "mid_events" and k == 16:
+                    e1.record(stream)
+            if how == "edge_events":
+                e1.record(stream)
+            torch.cuda.synchronize(dev)
+            xs.append(time.perf_counter() - t)
+        out[f"wall_20_{how}_us"] = med(xs)
     print(json.dumps(out))
 
 
