@@ -680,9 +680,7 @@ __device__ void env_dynamics(const State<R>& S, int e, float a_u, float a_r, flo
   int k0 = 0;                                        // f32: the heading's whole turns (store_heading)
   R pdl = R(0);                                      // f32 usv-asmc-simple: psi_d_last, phi's frame
   if constexpr (kF32) {
-#ifndef USV_AB_NO_REBASE
     k0 = S.I(I_TURNS)[e];
-#endif
     if constexpr (kAsmc && !CHAIN) pdl = S.asmc[e];
   }
   if (kAsmc) {
@@ -744,11 +742,7 @@ __device__ void env_dynamics(const State<R>& S, int e, float a_u, float a_r, flo
   }
   px = x; py = y;
   heading_sincos(psi, &psp, &pcp);
-#ifdef USV_AB_NO_REBASE
-  if constexpr (false) {                             // (A/B timing builds only: wrong for spinning envs)
-#else
   if constexpr (kF32) {                              // the rebase (see the heading representation)
-#endif
     // branch-free and stored unconditionally (n = 0 leaves both values unchanged, bit for bit): a
     // conditional store made the compiler sink the k0 load into its branch, and a wave with one
     // rebasing lane then waited a memory round trip in the middle of phase 1
@@ -2058,11 +2052,7 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
 #endif
   if (threadIdx.x == 0) *qctr = kQW;                   // pairs 0 .. kQW-1 are the static first ones
   // the ray table: by the last wave, so that the dynamics waves (fused) issue no DMA of their own
-#ifdef USV_P1_R3
-  if (wave == 0) dma_copy(S.ray_tab, lds, (int)wave_tab_bytes<float>());   // (A/B builds: round 3's phase 1)
-#else
   if (wave == kQW - 1) dma_copy(S.ray_tab, lds, (int)wave_tab_bytes<float>());
-#endif
 #pragma unroll
   for (int i = 0; i < 4; ++i) slot[i * 64 + l] = kSlotArm;
   mark[l] = 0;                                         // lidar_window2 clears them after each call
@@ -2087,9 +2077,7 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
     // wave wait for every store's ack (one vmcnt counter) before the barrier
     if (wave >= 2 * kDynWaves && wave < 3 * kDynWaves) {
       const int k = (wave - 2 * kDynWaves) * kWave + l;
-#ifndef USV_AB_NOB_LATE
       if (k < nbe) qnob[k] = S.I(I_NOBS)[eb + k];
-#endif
     }
     // dynamics, one lane per env.  Lanes past the end repeat the wave's last env (same wave:
     // every lane loads the state before any lane stores it); a wave with no env of its own must
@@ -2104,11 +2092,7 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
       env_dynamics<float, MODE, CHAIN>(S, e, a.x, a.y, hdr, px, py, sp, cp, partial, trunc,
                                        INFO ? io.info + (size_t)e * USV_INFO_DIM : nullptr);
       io.trunc[e] = trunc;
-#ifdef USV_AB_NOB_LATE
-      make_qrec(recs + k * kQRec, px, py, sp, cp, partial, S.I(I_NOBS)[e], trunc, hdr);
-#else
       make_qrec(recs + k * kQRec, px, py, sp, cp, partial, 0, trunc, hdr);   // (n_obs: qnob)
-#endif
     }
   } else {
     if (wave < kQE / 16 && wave * 16 < nbe)            // 16 records (1 KiB) per wave
@@ -2117,11 +2101,7 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
   // rows, ray table and records landed (the dynamics waves issued no DMA: their stores drain later,
   // ahead of their first pair's rows in the vmcnt order)
   USV_STAMP_W(1);
-#ifdef USV_P1_R3
-  vm_wait<0>();
-#else
   if (wave >= kDynWaves) vm_wait<0>();
-#endif
   QMARK(10);
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   USV_STAMP_W(2);
@@ -2161,9 +2141,7 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
     const float* const rk = recs + kk * kQRec;
     P = *reinterpret_cast<const float4*>(rk);
     M = *reinterpret_cast<const float4*>(rk + 4);
-#ifndef USV_AB_NOB_LATE
     if constexpr (FUSED) M.y = __int_as_float(__float_as_int(M.y) | qnob[kk]);   // n_obs | truncated << 16
-#endif
     if constexpr (!SPAN) {                             // (the constant entries are selected at the store)
       H = recs[((((hpk >> 16) & 1) && cB) ? c0 + 1 : c0) * kQRec + ((hpk >> 8) & 31)];
       return;
