@@ -200,7 +200,7 @@ def main():
     ap.add_argument("--cpu-procs", type=int, default=0, help="0 = every usable host core")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--event-every", type=int, default=16, help="launches per HIP-event-timed group (mid layout)")
-    ap.add_argument("--event-layout", default="edge", choices=["edge", "mid"],
+    ap.add_argument("--event-layout", default="mid", choices=["edge", "mid"],
                     help="edge: one event pair around all K timed launches; mid: groups inside the loop")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_summary.json"))
     ap.add_argument("--clock-warmup", type=float, default=0.3,
