@@ -16,8 +16,8 @@ otherwise time a cold chip).  The line reports both counts.
 
 Rank 0 prints one JSON line: value = all ranks' env-steps / max-rank time, plus
   roofline:     algorithmic bytes per launch / mean launch duration (HIP events on the env's stream
-                at both ends of the K timed launches; --event-layout mid: around launches 2..K-1 in
-                groups, the round-3 layout, whose timing markers between launches cost wall time)
+                around groups of back-to-back launches 2..K; --event-layout edge: one pair around
+                all K launches, no timing marker between two launches)
                 vs 8 TB/s; traffic from the committed
                 rocprofv3 PMC summary (profiles/pmc_summary.json) when it matches the workload;
                 valu_frac = VALU wave-instructions per launch (same summary, SQ_INSTS_VALU) x 2
