@@ -103,7 +103,13 @@ __device__ __forceinline__ void qprof_flush(QProf* qp) { qp->flush(); }
 #define QCOUNT(i, k) do { if (qp) qp->count(i, k); } while (0)
 #else
 struct QProf { __device__ void mark(int) {} __device__ void count(int, unsigned = 1) {} __device__ void flush() {} };
+#ifdef USV_DIAG_SECTIONS
+// (-DUSV_DIAG_SECTIONS, assembly listings only: a comment per section boundary for
+// tools/section_mix.py's static instruction mix of the block-queue loop)
+#define QMARK(i) asm volatile(";@@QMARK " #i)
+#else
 #define QMARK(i) do {} while (0)
+#endif
 #define QCOUNT(i, k) do {} while (0)
 __device__ __forceinline__ void qprof_flush(QProf*) {}
 #endif
