@@ -92,6 +92,23 @@ def aggregate_rate(envs_per_rank, world, steps, max_elapsed):
     return envs_per_rank * world * steps / max_elapsed
 
 
+def timed_window(launch, K, sync, barrier):
+    """The timed region: sync, barrier, sync, then t0; K launches; sync, then t1.  The barrier
+    lines the ranks up before t0, and nothing between t0 and t1 is a collective: the max over ranks
+    (reduce_max) and the closing barrier come after t1, so an N-rank curve times kernels, not RCCL
+    (tests/test_multirank.py::test_timed_window_is_collective_free)."""
+    sync()
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    for k in range(K):
+        launch(k)
+    sync()
+    t1 = time.perf_counter()
+    barrier()          # (outside the window) every rank has finished before the reductions
+    return t0, t1
+
+
 # --------------------------------------------------------------------------- CPU baseline
 def _cpu_worker(args):
     env_id, seconds, seed = args
@@ -185,6 +202,68 @@ def cpu_baseline(env_id, seconds, procs, affinity=None, quota=None):
     return out
 
 
+# --------------------------------------------------------------------------- reference precision
+def pmc_entry(path, key):
+    """(traffic bytes per launch, SQ_INSTS_VALU per launch) of `key` in the committed PMC summary."""
+    try:
+        d = json.load(open(path)).get(key)
+    except (OSError, ValueError):
+        return None, None
+    if not d:
+        return None, None
+    return d.get("hbm_bytes_per_launch"), d.get("sq_insts_valu_per_launch")
+
+
+def f64_leg(args, N, rank, dev, stream, acts, pool):
+    """The default float64 step kernel (the reference's precision) on the same env count and
+    actions: env-steps/s and the roofline from one HIP event pair around --f64-steps back-to-back
+    launches (after --warmup + 64 untimed ones)."""
+    import ctypes
+    import torch
+    import gym_usv_amd
+    env = gym_usv_amd.make_vec(args.env_id, N, device=dev.index, seed=args.seed, precision="f64",
+                               lidar=args.lidar, env_id_offset=shard(rank, N)[0])
+    env.reset(seed=args.seed)
+    mean_obs = float(env.get_field("n_obs").mean())
+    D = env.obs_dim
+    obs = torch.empty((N, D), device=dev)
+    fobs = torch.empty((N, D), device=dev)
+    rew = torch.empty(N, device=dev, dtype=torch.float64)
+    term = torch.empty(N, device=dev, dtype=torch.uint8)
+    trunc = torch.empty(N, device=dev, dtype=torch.uint8)
+    vp = ctypes.c_void_p
+    outs = (vp(obs.data_ptr()), vp(rew.data_ptr()), vp(term.data_ptr()), vp(trunc.data_ptr()),
+            vp(fobs.data_ptr()), vp(stream.cuda_stream))
+    bound = [(env._h, vp(acts[i].data_ptr())) + outs for i in range(pool)]
+    step_fn = env.lib.usv_step
+
+    def launch(k):
+        rc = step_fn(*bound[k % pool])
+        if rc != 0:
+            raise RuntimeError(env.lib.usv_last_error().decode())
+    for k in range(args.warmup + 64):
+        launch(k)
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record(stream)
+    for k in range(args.f64_steps):
+        launch(k)
+    b.record(stream)
+    b.synchronize()
+    ms = a.elapsed_time(b) / args.f64_steps
+    env.close()
+    bpe = algorithmic_bytes_per_env_step(args.env_id, mean_obs, "f64")
+    achieved = bpe * N / (ms * 1e-3) / 1e9
+    traffic, valu = pmc_entry(args.pmc, f"{args.env_id}/{N}/f64/{args.lidar}")
+    return {"dtype": "f64", "env_steps_per_s": round(N / (ms * 1e-3), 1), "kernel_ms": round(ms, 5),
+            "launches": args.f64_steps, "mean_obstacles": round(mean_obs, 2),
+            "algorithmic_bytes_per_env_step": round(bpe, 1), "achieved": round(achieved, 1),
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+            "valu_frac": (round(valu * VALU_CYCLES / (SIMDS * CLOCK_GHZ * 1e9 * ms * 1e-3), 4) if valu else None),
+            "note": "the default float64 step kernel (the reference's arithmetic, bit-exact obs parity) on the "
+                    "same env count and actions; one HIP event pair around that many launches, untimed by "
+                    "the contract; traffic from profiles/pmc_summary.json"}
+
+
 # --------------------------------------------------------------------------- main
 def main():
     ap = argparse.ArgumentParser()
@@ -205,6 +284,10 @@ def main():
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_summary.json"))
     ap.add_argument("--clock-warmup", type=float, default=0.3,
                     help="untimed steps after --warmup until this many seconds have passed")
+    ap.add_argument("--steady-steps", type=int, default=1000,
+                    help="untimed launches after the timed region for roofline.steady (0 = skip)")
+    ap.add_argument("--f64-steps", type=int, default=500,
+                    help="launches of the f64 (reference-precision) leg after the timed region (0 = skip)")
     ap.add_argument("--api-steps", type=int, default=200, help="steps of the public-API leg (0 = skip)")
     ap.add_argument("--variant", default=None, help="step-kernel variant epb,lid,kind (tools; default: tuned)")
     args = ap.parse_args()
@@ -280,37 +363,50 @@ def main():
     for a, b in ev:                                   # the events exist before the timed region
         a.record(stream)
         b.record(stream)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    if edge:
-        # one timing marker before the first launch and one after the last: a marker between two
-        # launches makes the second wait for the first's end-of-kernel release (tools/probe_wall.py)
-        ev[0][0].record(stream)
-        for k in range(K):
+
+    def timed_launch(k):
+        if edge:
+            # one timing marker before the first launch and one after the last: a marker between two
+            # launches makes the second wait for the first's end-of-kernel release (tools/probe_wall.py)
+            if k == 0:
+                ev[0][0].record(stream)
             launch(W2 + k)
-        ev[0][1].record(stream)
-    else:
-        launch(W2)
-        for k in range(1, K):
-            g, r = divmod(k - 1, G)
-            if g < groups and r == 0:
-                ev[g][0].record(stream)
-            launch(W2 + k)
-            if g < groups and r == G - 1:
-                ev[g][1].record(stream)
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
+            if k == K - 1:
+                ev[0][1].record(stream)
+            return
+        g, r = divmod(k - 1, G)
+        if k > 0 and g < groups and r == 0:
+            ev[g][0].record(stream)
+        launch(W2 + k)
+        if k > 0 and g < groups and r == G - 1:
+            ev[g][1].record(stream)
+
+    t0, t1 = timed_window(timed_launch, K, lambda: torch.cuda.synchronize(dev),
+                          dist.barrier if world > 1 else (lambda: None))
+    elapsed = t1 - t0
     if edge:
         kern_ms = ev[0][0].elapsed_time(ev[0][1]) / K
     else:
         kern_ms = (sum(a.elapsed_time(b) for a, b in ev) / (groups * G)) if groups else elapsed / K * 1e3
-    elapsed, kern_ms = reduce_max([elapsed, kern_ms], device=dev)
+    # steady-state kernel time (after the timed region, untimed by the contract): one event pair
+    # around --steady-steps more back-to-back launches, so the roofline is not read off a single
+    # 16-launch group when the driver runs --steps 20
+    steady_ms = None
+    if args.steady_steps > 0:
+        sa, sb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        sa.record(stream)
+        for k in range(args.steady_steps):
+            launch(W2 + K + k)
+        sb.record(stream)
+        sb.synchronize()
+        steady_ms = sa.elapsed_time(sb) / args.steady_steps
+    elapsed, kern_ms, steady_ms = reduce_max([elapsed, kern_ms, steady_ms or 0.0], device=dev)
+
+    # the reference's precision (float64, simple_env.py:32-54) on the same workload, untimed by the
+    # contract: its own env and the same launch path, one event pair around --f64-steps launches
+    f64 = None
+    if args.f64_steps > 0 and args.precision == "f32" and args.env_id not in LEGACY_IDS:
+        f64 = f64_leg(args, N, rank, dev, stream, acts, pool)
 
     # public API leg (untimed by the contract above): UsvVectorEnv.step on the same envs
     api = None
@@ -337,23 +433,14 @@ def main():
         bpe = algorithmic_bytes_per_env_step(args.env_id, mean_obs, args.precision)
         bytes_per_launch = bpe * N
         achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
-        traffic = valu = None
-        if os.path.exists(args.pmc):
-            try:
-                pmc = json.load(open(args.pmc))
-                key = f"{args.env_id}/{N}/{args.precision}/{args.lidar}"
-                if key in pmc:
-                    traffic = pmc[key]["hbm_bytes_per_launch"]
-                    valu = pmc[key].get("sq_insts_valu_per_launch")
-            except Exception:
-                traffic = valu = None
+        traffic, valu = pmc_entry(args.pmc, f"{args.env_id}/{N}/{args.precision}/{args.lidar}")
         valu_frac = None
         if valu:
             valu_frac = round(valu * VALU_CYCLES / (SIMDS * CLOCK_GHZ * 1e9 * kern_ms * 1e-3), 4)
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world,
             "steps": K, "warmup": W, "clock_warmup_steps": extra, "ms_per_step": round(elapsed / K * 1e3, 5),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "ranks_seen": world,
             "dtype": args.precision, "data": "synthetic (on-device uniform random actions, Philox env resets)",
             "config": {"workload": f"C3: {args.env_id}, {N} envs per GPU, random-action rollout, "
                                    f"in-kernel TimeLimit + same-step autoreset",
@@ -367,9 +454,14 @@ def main():
                                            f"HIP events around {groups} group(s) of {G} launches"),
                          "algorithmic_bytes_per_env_step": round(bpe, 1),
                          "valu_frac": valu_frac,
+                         "steady": ({"kernel_ms": round(steady_ms, 5), "launches": args.steady_steps,
+                                     "frac": round(bytes_per_launch / (steady_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                                     "timing": "one HIP event pair around that many back-to-back launches "
+                                               "after the timed region"} if steady_ms else None),
                          "valu_basis": "SQ_INSTS_VALU per launch (profiles/pmc_summary.json) x 2 cycles / "
                                        "(1024 SIMDs x 2.4 GHz x kernel_ms)" if valu_frac is not None else None},
             "api_step": api,
+            "f64": f64,
         }
         if args.env_id in LEGACY_IDS:
             out["config"].pop("lidar")

@@ -395,6 +395,102 @@ __device__ __forceinline__ void asmc_substep(R (&s)[kAsmcN], R a0, R a1, R& x, R
 //    read inside the substep, so xl, yl accumulate their increments and the caller adds them after the
 //    20 substeps; psi is read by the next substep, so it integrates with compensated summation (pl
 //    carries what each addition rounded away; golden replay reward error 1.0e-4 -> 3.5e-5).
+#ifndef USV_ASMC_F32_V1
+// asin on [-1, 1] for the f32 substep: |x| < 1/2 as s + s t P(t) with t = x^2, else
+// pi/2 - 2 asin(sqrt((1 - |x|) / 2)) with the same polynomial (Cephes asinf's minimax P, ~2.5e-7
+// relative); one hardware sqrt, both arms branch-free
+__device__ __forceinline__ float asin_f32(float x) {
+  const float ax = fabsf(x);
+  const bool big = ax >= 0.5f;
+  const float t = big ? fmaf(-0.5f, ax, 0.5f) : x * x;
+  const float s = big ? __builtin_amdgcn_sqrtf(t) : ax;
+  const float p = fmaf(fmaf(fmaf(fmaf(4.2163199048e-2f, t, 2.4181311049e-2f), t, 4.5470025998e-2f), t,
+                            7.4953002686e-2f), t, 1.6666752422e-1f);
+  const float as = fmaf(s * t, p, s);
+  return copysignf(big ? fmaf(-2.0f, as, 1.57079632679f) : as, x);
+}
+
+// Round 5: the rhs of M nu' = tau - C(nu) nu - D(nu) nu folded further (identities in real arithmetic,
+// with (Tx, 0, Tz) as in round 4):
+//  * surge: M00 = m - Xu', so u' = (lambda_u e_u - ua_u) - (Yv' v r + (Yr' + Nv') r^2 + Xuu |u| (1 - u)) / M00
+//    (f_u's and C's v r terms and D's Xu u cancel: the reference's f_u carries Xuu |u| + Xu u, :113);
+//  * yaw: tau_z's -Nr r cancels D's Nr-linear part (:108, :213-223), and the u v terms of tau_z and
+//    C(nu) are one coefficient;
+//  * np.sign(|sigma| - mu) at exactly 0 is not kept (the f32 equality is not the reference's float64
+//    one anyway);  asin as asin_f32 above.
+// The f32 substep is held to SURVEY 8(c)'s tolerance, not to the reference's rounding.
+__device__ __forceinline__ void asmc_substep_f32(float (&s)[kAsmcN], float a0, float a1, float& x, float& y,
+                                                 float& psi, float& u, float& v, float& r, float& xl, float& yl,
+                                                 float& pl, float kt, int pstep = 0, bool perturb = false) {
+  constexpr float h2 = float(H / 2);
+  const float au = fabsf(u), av = fabsf(v), ar = fabsf(r);
+  const float vmag = __builtin_amdgcn_sqrtf(fmaf(u, u, v * v));
+  // yaw channel: LOS heading, third-order filter, sliding surface (:72-89, :119-121, :134)
+  const float beta = asin_f32(v * __builtin_amdgcn_rcpf(0.001f + vmag));
+  const float psi_d = psi + beta + a1;
+  const float r_d = (psi_d - s[0]) * float(1.0 / H);
+  s[0] = psi_d;
+  const float o_dd = 4.0f * ((r_d - s[1]) - s[2]);
+  const float o_d = fmaf(o_dd + s[3], h2, s[2]);
+  const float o = fmaf(o_d + s[2], h2, s[1]);
+  s[1] = o; s[2] = o_d; s[3] = o_dd;
+  const float e_psi = asmc_wrap(psi_d - psi);
+  const float sig_p = (o - r) + float(LAMBDA_PSI) * e_psi;
+  // surge channel (:128-133)
+  const float e_u = a0 - u;
+  s[13] = fmaf(e_u + s[10], h2, s[13]);
+  s[10] = e_u;
+  const float sig_u = fmaf(float(LAMBDA_U), s[13], e_u);
+  // adaptive gains (:137-146) and control laws (:150-151)
+  const float kdu = s[14] > float(KMIN_U) ? copysignf(float(K_U), fabsf(sig_u) - float(MU_U)) : float(KMIN_U);
+  const float kdp = s[15] > float(KMIN_PSI) ? copysignf(float(K_PSI), fabsf(sig_p) - float(MU_PSI)) : float(KMIN_PSI);
+  s[14] = fmaf(kdu + s[11], h2, s[14]);
+  s[15] = fmaf(kdp + s[12], h2, s[15]);
+  s[11] = kdu; s[12] = kdp;
+  const float au_u = fmaf(float(K2_U), sig_u, fmaf(float(LAMBDA_U), e_u,
+                          s[14] * copysignf(__builtin_amdgcn_sqrtf(fabsf(sig_u)), sig_u)));   // lambda e - ua
+  const float au_p = fmaf(float(K2_PSI), sig_p, fmaf(float(LAMBDA_PSI), e_psi,
+                          s[15] * copysignf(__builtin_amdgcn_sqrtf(fabsf(sig_p)), sig_p)));
+  // J(psi_old) (:179), psi reduced by the env step's whole turns kt (see the round-4 note above)
+  const float pr = fmaf(kt, 1.74845553e-07f, fmaf(-kt, 6.28318548f, psi));
+  const float sp = __sinf(pr), cp = __cosf(pr);
+  float p0 = 0.0f, p1 = 0.0f;
+  if (perturb) {                                                                // T += F @ J (:184-198)
+    double fx, fy;
+    perturb_force(pstep, fx, fy);
+    const float pfx = float(fx), pfy = float(fy);
+    p0 = pfx * cp + pfy * sp;
+    p1 = pfx * -sp + pfy * cp;
+  }
+  const float xuu = au > 1.2f ? -70.92f : 0.0f;                                 // :95-99 (Xu cancels)
+  const float qs = fmaf(xuu * au, 1.0f - u, fmaf(float(Y_R_DOT + N_V_DOT), r, float(Y_V_DOT) * v) * r);
+  const float ud = fmaf(float(MI00), p0 - qs, au_u);                            // :226
+  const float md11 = fmaf(float(YV_K + YVV), av, float(YVR) * ar);
+  const float md12 = fmaf(float(YR_K), vmag, fmaf(float(YRV), av, float(YRR) * ar));
+  const float md21 = fmaf(float(NV_K), vmag, fmaf(float(NVV), av, float(NVR) * ar));
+  const float n22 = fmaf(float(NRV), av, float(NRR) * ar);
+  const float rhs1 = fmaf(md11, v, fmaf(fmaf(float(-(MASS - X_U_DOT * MASS)), u, md12), r, p1));
+  const float rhs2 = fmaf(float(IZ - N_R_DOT), au_p,
+                          fmaf(u, fmaf(float(X_U_DOT + Y_V_DOT - X_U_DOT * MASS), v, float(Y_R_DOT + N_V_DOT) * r),
+                               fmaf(md21, v, n22 * r)));
+  const float vd = fmaf(float(MI11), rhs1, float(MI12) * rhs2);
+  const float rd = fmaf(float(MI21), rhs1, float(MI22) * rhs2);
+  u = fmaf(ud + s[7], h2, u);                                                   // :228-229
+  v = fmaf(vd + s[8], h2, v);
+  r = fmaf(rd + s[9], h2, r);
+  s[7] = ud; s[8] = vd; s[9] = rd;
+  const float xd = fmaf(cp, u, -(sp * v)), yd = fmaf(sp, u, cp * v);          // :233
+  {                                                                             // :234
+    const float ix = (xd + s[4]) * h2, iy = (yd + s[5]) * h2, ip = (r + s[6]) * h2;
+    xl += ix;
+    yl += iy;
+    const float sq = psi + ip;
+    pl += ip - (sq - psi);
+    psi = sq;
+  }
+  s[4] = xd; s[5] = yd; s[6] = r;
+}
+#else
 __device__ __forceinline__ void asmc_substep_f32(float (&s)[kAsmcN], float a0, float a1, float& x, float& y,
                                                  float& psi, float& u, float& v, float& r, float& xl, float& yl,
                                                  float& pl, float kt, int pstep = 0, bool perturb = false) {
@@ -476,5 +572,6 @@ __device__ __forceinline__ void asmc_substep_f32(float (&s)[kAsmcN], float a0, f
   }
   s[4] = xd; s[5] = yd; s[6] = r;
 }
+#endif
 
 }  // namespace usv

@@ -1597,10 +1597,12 @@ __device__ __forceinline__ void emit_env(const State<R>& S, const IO<R>& io, int
 // P = (x, y, sin psi, cos psi), obstacle count nl, truncation bits trunc_m.  Writes the sensor
 // half of each obs row, final obs and stale scan of done envs; returns term / collision bits.
 // Precondition: the prologue DMAs have landed and the ray table is published.
+// sig (kind 3, wave 0): set to 1 once every memory op issued before the scan (the block's dynamics
+// stores) is complete.
 template <typename R, int MODE, int LID>
 __device__ __forceinline__ void scan_envs(const State<R>& S, const IO<R>& io, const ScanLds<R>& L, int e0,
                                           int ne, const R4<R>& P, int nl, unsigned trunc_m,
-                                          unsigned& term_m, unsigned& coll_m, Prof& prof) {
+                                          unsigned& term_m, unsigned& coll_m, Prof& prof, unsigned* sig = nullptr) {
   const int cap = S.cap;
   const int rowb = row_bytes<R>(cap);
   const int step = scan_step<R, LID>(cap);
@@ -1618,6 +1620,7 @@ __device__ __forceinline__ void scan_envs(const State<R>& S, const IO<R>& io, co
     // sensor-row stores after their DMA (a full pair: four), so all older ops are done
     if (k > 0) {
       if (step == 2) vm_wait<4>(); else vm_wait<2>();
+      if (sig && k == step) *sig = 1u;
     }
     if (k + step < ne)
       dma_copy(S.orow(e0 + k + step), ((k / step) & 1) ? L.row0 : L.row1, min(step, ne - k - step) * rowb);
@@ -1673,14 +1676,20 @@ __device__ __forceinline__ void scan_envs(const State<R>& S, const IO<R>& io, co
     emit(k, sc);
     prof.mark(3);
   }
+  if (sig && ne <= step) {                         // (one iteration: no wait above)
+    vm_wait<0>();
+    *sig = 1u;
+  }
 }
 
 // Epilogue shared by both: terminated flag and collision term of the reward (lane-per-env),
 // then same-step autoreset of the done envs.
+// dynsig (kind 3): the flag scan_envs(sig) sets on the wave that ran this env's dynamics; a reset
+// waits for it, so the dynamics' state stores cannot land after the reset's.
 template <typename R, int MODE>
 __device__ __forceinline__ void scan_epilogue(const State<R>& S, const IO<R>& io, int e0, int ne,
                                               R partial, bool have_partial, unsigned term_m,
-                                              unsigned coll_m, unsigned trunc_m) {
+                                              unsigned coll_m, unsigned trunc_m, const unsigned* dynsig = nullptr) {
   const int l = lane_id();
   if (l < ne) {
     const int e = e0 + l;
@@ -1692,6 +1701,9 @@ __device__ __forceinline__ void scan_epilogue(const State<R>& S, const IO<R>& io
     if (io.done) io.done[e] = ((term_m | trunc_m) >> l) & 1;
   }
   if (S.autoreset == USV_AUTORESET_SAME_STEP) {
+    if (dynsig && (term_m | trunc_m))
+      while (__hip_atomic_load(dynsig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
+        __builtin_amdgcn_s_sleep(2);
     for (int k = 0; k < ne; ++k)
       if (((term_m | trunc_m) >> k) & 1) reset_wave<R, MODE>(S, e0 + k, io.obs + (size_t)(e0 + k) * kObsDim);
   }
@@ -1836,7 +1848,7 @@ void scan_kernel_d(State<R> S, IO<R> io) { scan_body<R, MODE, EPW, LID, WPB>(S, 
 // flight.  Same per-env arithmetic as kinds 1 and 2, one launch instead of two (no pose records
 // through HBM, no second launch ramp).
 template <typename R> __host__ __device__ constexpr size_t lds_blockdyn_bytes(int cap) {
-  return (lds_scan_bytes<R>(cap) + 31) / 32 * 32 + 2 * kWave * sizeof(R4<R>);
+  return (lds_scan_bytes<R>(cap) + 31) / 32 * 32 + 2 * kWave * sizeof(R4<R>) + 16;   // + wave 0's store flag
 }
 template <typename R, int MODE, int EPW, int LID>
 __device__ __forceinline__ void step_body_blockdyn(const State<R>& S, const IO<R>& io) {
@@ -1850,6 +1862,8 @@ __device__ __forceinline__ void step_body_blockdyn(const State<R>& S, const IO<R
   const int ne = min(EPW, S.N - e0);
   const ScanLds<R> L = scan_lds<R>(lds, wave, S.cap);
   R4<R>* const rec = reinterpret_cast<R4<R>*>(lds + (lds_scan_bytes<R>(S.cap) + 31) / 32 * 32);
+  unsigned* const dynsig = reinterpret_cast<unsigned*>(rec + 2 * kWave);   // wave 0's stores complete
+  if (threadIdx.x == 0) *dynsig = 0u;
   Prof prof;
   USV_STAMP_W(0);
   USV_STAMP_ID();
@@ -1884,16 +1898,23 @@ __device__ __forceinline__ void step_body_blockdyn(const State<R>& S, const IO<R
     vm_wait<0>();
   }
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // records + ray table published
-  if (ne <= 0) return;
+  if (ne <= 0) {
+    if (wave == 0) {                                  // (no envs of its own to scan)
+      vm_wait<0>();
+      *dynsig = 1u;
+    }
+    return;
+  }
   USV_STAMP_W(2);
   prof.mark(0);
   const int k = wave * EPW + min(l, ne - 1);                // lane-per-env view of this wave's envs
   const R4<R> P = rec[k], M = rec[kWave + k];
   const unsigned trunc_m = (unsigned)ballot(M.z != R(0));
   unsigned term_m, coll_m;
-  scan_envs<R, MODE, LID>(S, io, L, e0, ne, P, (int)M.y, trunc_m, term_m, coll_m, prof);
+  scan_envs<R, MODE, LID>(S, io, L, e0, ne, P, (int)M.y, trunc_m, term_m, coll_m, prof,
+                          wave == 0 ? dynsig : nullptr);
   USV_STAMP_W(3);
-  scan_epilogue<R, MODE>(S, io, e0, ne, M.x, true, term_m, coll_m, trunc_m);
+  scan_epilogue<R, MODE>(S, io, e0, ne, M.x, true, term_m, coll_m, trunc_m, wave == 0 ? nullptr : dynsig);
   prof.mark(5);
   prof.flush(blockIdx.x * kWaves + wave);
   USV_STAMP_W(6);
@@ -1930,6 +1951,15 @@ void step_kernel_blockdyn(State<R> S, IO<R> io) { step_body_blockdyn<R, MODE, EP
 #endif
 #ifndef USV_QWPE
 #define USV_QWPE 8       // waves per SIMD it is compiled for
+#endif
+#ifndef USV_QPRIO_DYN
+#define USV_QPRIO_DYN 0  // experiment: issue priority of the dynamics waves in phase 1 (0: default)
+#endif
+#ifndef USV_QPRIO_YOUNG
+#define USV_QPRIO_YOUNG 0  // experiment: second-slot blocks raise waves 0 .. this - 1 to priority USV_QPRIO_YLVL
+#endif
+#ifndef USV_QPRIO_YLVL
+#define USV_QPRIO_YLVL 1
 #endif
 constexpr int kQW = USV_QW, kQE = USV_QE, kQRec = 16;
 __host__ __device__ constexpr size_t q_slice_bytes() { return 256 * 8 + 64 * 4 + 2 * 1024; }
@@ -2050,7 +2080,14 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
 #else
   QProf* const qp = nullptr;
 #endif
-  if (threadIdx.x == 0) *qctr = kQW;                   // pairs 0 .. kQW-1 are the static first ones
+  // qctr[1 + w]: dynamics wave w's state stores are complete (fused, same-step autoreset: a wave
+  // that resets an env of wave w's first, so its reset stores cannot be overtaken by them)
+  unsigned* const qdyn = qctr + 1;
+  if (threadIdx.x == 0) {
+    qctr[0] = kQW;                                     // pairs 0 .. kQW-1 are the static first ones
+    qdyn[0] = 0u;
+    qdyn[1] = 0u;
+  }
   // the ray table: by the last wave, so that the dynamics waves (fused) issue no DMA of their own
   if (wave == kQW - 1) dma_copy(S.ray_tab, lds, (int)wave_tab_bytes<float>());
 #pragma unroll
@@ -2083,6 +2120,9 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
     // every lane loads the state before any lane stores it); a wave with no env of its own must
     // not run, or two waves would race on the same env's state
     if (wave < kDynWaves && wave * kWave < nbe) {
+#if USV_QPRIO_DYN
+      __builtin_amdgcn_s_setprio(USV_QPRIO_DYN);
+#endif
       const int k = min(wave * kWave + l, nbe - 1);
       const int e = eb + k;
       const float2 a = reinterpret_cast<const float2*>(io.act)[e];
@@ -2104,6 +2144,12 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
   if (wave >= kDynWaves) vm_wait<0>();
   QMARK(10);
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#if USV_QPRIO_DYN
+  if (FUSED && wave < kDynWaves) __builtin_amdgcn_s_setprio(0);
+#endif
+#if USV_QPRIO_YOUNG
+  if (2 * blockIdx.x >= gridDim.x && wave < USV_QPRIO_YOUNG) __builtin_amdgcn_s_setprio(USV_QPRIO_YLVL);
+#endif
   USV_STAMP_W(2);
   QMARK(0);
   unsigned tk = 0;
@@ -2250,6 +2296,8 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
       QMARK(5);
       vm_wait<7>();
       QMARK(6);
+      // every memory op before this pair's DMA is complete, the phase-1 state stores included
+      if (FUSED && wave < kDynWaves) qdyn[wave] = 1u;
       if (it == 0) USV_STAMP_W(5);                      // (diagnostic: first pair done)
       cur = nxt;
       pose = pose_n;
@@ -2266,11 +2314,22 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
     QMARK(11);
     for (; done; done &= done - 1) {
       const int e = de0 + __builtin_ctz(done);
+      if constexpr (FUSED) {
+        // the env's phase-1 stores (by dynamics wave (e - eb) / 64) are acknowledged before its reset
+        // stores are issued: two waves' stores to one address are otherwise unordered
+        const unsigned* const f = qdyn + ((e - eb) >> 6);
+        while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
+          __builtin_amdgcn_s_sleep(2);
+      }
       reset_wave<float, MODE>(S, e, io.obs + (size_t)e * kObsDim);
     }
     QMARK(7);
   }
   QMARK(11);
+  if (FUSED && wave < kDynWaves) {                     // (a dynamics wave that scanned no pair)
+    vm_wait<0>();
+    qdyn[wave] = 1u;
+  }
   qprof_flush(qp);
   USV_STAMP_V(4, (unsigned long long)it);            // (diagnostic: pairs this wave scanned)
   USV_STAMP_W(3);
@@ -3107,7 +3166,12 @@ int heading_io(Handle* h, State<R>& S, int f, double* hd, bool to_host) {
     HIP_TRY(hipMemcpy(dev, t.data(), N * sizeof(R), hipMemcpyHostToDevice));
     return USV_OK;
   }
-  // a new heading: new whole turns, and usv-asmc-simple's psi_d_last moved into the new frame
+  // a new heading: new whole turns, and usv-asmc-simple's psi_d_last moved into the new frame.
+  // The turn count is an int32: a non-finite heading, or one whose turns do not fit (|psi| beyond
+  // about 1.3e10 rad), is refused before anything is written.
+  for (size_t e = 0; e < N; ++e)
+    if (!std::isfinite(hd[e]) || std::fabs(hd[e] / kTwoPi) > 2147483000.0)
+      return fail(USV_ERR_ARG, "heading must be finite with |psi| / 2 pi < 2^31");
   std::vector<int32_t> kn(N);
   for (size_t e = 0; e < N; ++e) {
     const double n = std::nearbyint(hd[e] / kTwoPi);

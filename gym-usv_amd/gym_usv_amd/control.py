@@ -2,8 +2,10 @@
 
 ``UsvAsmc`` keeps the reference's single-controller API -- ``compute(action, position, velocity,
 do_perturb) -> (position, velocity, infos)`` on NumPy 3-vectors, and the ``so_filter`` (7),
-``last`` (9), ``aux_vars`` (3) and ``perturb_step`` attributes (:43-49) -- so the reference's own
-tests (tests/test_usv_asmc.py:8-37) run against it.  ``UsvAsmcBatch`` is the batched form: n
+``last`` (9), ``aux_vars`` (3) and ``perturb_step`` attributes (:43-49).  The reference's own tests
+(tests/test_usv_asmc.py:8-37) call ``compute(a, p, v)`` and unpack two results, which the reference's
+own ``compute`` (four arguments, three results) does not accept either; tests/test_gpu_r4.py runs
+them in the adapted form ``p, v, _ = compute(a, p, v, False)``, as SURVEY §4 states.  ``UsvAsmcBatch`` is the batched form: n
 independent controllers stepped in place on device tensors by one ``usv_asmc_compute`` launch.
 
 Precision: "f64" (default, the reference's float64 arithmetic, the same substep function as the

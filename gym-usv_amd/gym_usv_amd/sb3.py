@@ -28,8 +28,11 @@ The step itself stays on the GPU; only the arrays SB3 consumes are copied to the
 page-locked buffers: the stacked obs on a copy stream while the host builds the done envs' infos,
 the small arrays (reward, done) first, and the terminal rows of the done envs only.  The returned
 arrays alternate between two such buffer sets, so each stays valid until the second-next step
-(SB3's collectors consume or copy them within one step).  ``infos`` entries of envs that did not end
-are shared empty dicts (DummyVecEnv builds 4096 fresh ones per step: ~0.25 ms of Python).
+(SB3's collectors consume or copy them within one step).  ``infos`` is a fresh list of fresh dicts
+every step, as DummyVecEnv returns (a wrapper may write into them); the 4096 empty dicts are built
+while the GPU runs the step and the copies, so they cost no wall time on top of the copy wait.
+The env's device is the current device for the whole call (events and copies are ordered on its
+stream even when another device is current in the caller).
 """
 from __future__ import annotations
 
@@ -130,9 +133,6 @@ class Sb3VecEnv:
         self._act_dev = torch.empty((n, venv.act_dim), dtype=torch.float32, device=dev)
         self._rew32 = torch.empty(n, dtype=torch.float32, device=dev)
         self._copy_stream = torch.cuda.Stream(dev) if self._cuda else None
-        self._empty = [{} for _ in range(n)]           # infos of envs that did not end (shared)
-        self._infos = list(self._empty)
-        self._filled = np.empty(0, dtype=np.int64)
 
     # ---------------------------------------------------------------- VecEnv API
     def reset(self):
@@ -148,6 +148,12 @@ class Sb3VecEnv:
         self._actions = actions
 
     def step_wait(self):
+        if self._cuda:
+            with torch.cuda.device(self.venv.device):
+                return self._step_wait()
+        return self._step_wait()
+
+    def _step_wait(self):
         venv, n, dev = self.venv, self.num_envs, self.venv.device
         np.copyto(self._act_host.numpy(), np.asarray(self._actions, dtype=np.float32).reshape(n, -1))
         self._act_dev.copy_(self._act_host, non_blocking=self._cuda)
@@ -170,8 +176,9 @@ class Sb3VecEnv:
         self._hb ^= 1
         if self._cuda:
             # the stacked obs (the big copy) on the copy stream, overlapping the rest of this call
+            main = torch.cuda.current_stream(dev)
             ready = torch.cuda.Event()
-            ready.record()
+            ready.record(main)
             cs = self._copy_stream
             cs.wait_event(ready)
             with torch.cuda.stream(cs):
@@ -183,15 +190,15 @@ class Sb3VecEnv:
             h["rew"].copy_(self._rew32, non_blocking=True)
             h["done"].copy_(done, non_blocking=True)
             small = torch.cuda.Event()
-            small.record()
+            small.record(main)
+            infos = [{} for _ in range(n)]              # (built while the GPU works)
             small.synchronize()
         else:
             h["obs"].copy_(obs)
             h["rew"].copy_(rew)
             h["done"].copy_(done)
+            infos = [{} for _ in range(n)]
         done_np = h["done"].numpy()
-        for i in self._filled:                          # last step's done envs: back to empty infos
-            self._infos[i] = self._empty[i]
         idx = np.flatnonzero(done_np)
         if idx.size:
             ti = torch.from_numpy(idx).to(dev)
@@ -205,12 +212,11 @@ class Sb3VecEnv:
             t = round(time.time() - self._t0, 6)
             term_obs = pack[:, :w].astype(np.float32)
             for j, i in enumerate(idx):
-                self._infos[i] = {"terminal_observation": term_obs[j], "TimeLimit.truncated": bool(pack[j, w]),
+                infos[i] = {"terminal_observation": term_obs[j], "TimeLimit.truncated": bool(pack[j, w]),
                                   "episode": {"r": round(float(pack[j, w + 1]), 6), "l": int(pack[j, w + 2]), "t": t}}
-        self._filled = idx
         if self._cuda:
             obs_done.synchronize()
-        return h["obs"].numpy(), h["rew"].numpy(), done_np, list(self._infos)
+        return h["obs"].numpy(), h["rew"].numpy(), done_np, infos
 
     def step(self, actions):
         self.step_async(actions)

@@ -45,3 +45,57 @@ def test_two_rank_gloo_sharding_and_timing():
     for r in res:
         assert r[3] == 2.0 and r[4] == 1.0                                # max over ranks
         assert r[5] == pytest.approx(1000 * 2 * 10 / 2.0)                 # all ranks' env-steps / slowest
+
+
+def _window_worker(rank, world, port, q):
+    """bench.timed_window under gloo with every torch.distributed collective wrapped by a counter
+    that stamps perf_counter(): none may fall inside [t0, t1]."""
+    import time
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    calls = []
+    names = ("barrier", "all_reduce", "all_gather", "broadcast", "reduce", "all_gather_object",
+             "all_to_all", "reduce_scatter", "gather", "scatter", "monitored_barrier")
+    orig = {n: getattr(dist, n) for n in names if hasattr(dist, n)}
+
+    def wrap(n, f):
+        def g(*a, **k):
+            calls.append((n, time.perf_counter()))
+            return f(*a, **k)
+        return g
+    for n, f in orig.items():
+        setattr(dist, n, wrap(n, f))
+    launches = []
+
+    def launch(k):
+        launches.append(time.perf_counter())
+        time.sleep(0.002 * (1 + rank))          # ranks of different speed
+    try:
+        t0, t1 = bench.timed_window(launch, 5, lambda: None, dist.barrier)
+        el, = bench.reduce_max([t1 - t0])
+    finally:
+        for n, f in orig.items():
+            setattr(dist, n, f)
+    inside = [c for c in calls if t0 <= c[1] <= t1]
+    q.put((rank, len(launches), inside, [c[0] for c in calls], t1 - t0, el))
+    dist.destroy_process_group()
+
+
+def test_timed_window_is_collective_free():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_window_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    for rank, nl, inside, names, mine, el in res:
+        assert nl == 5
+        assert inside == [], f"rank {rank}: collectives inside the timed window: {inside}"
+        assert names.count("barrier") == 2 and "all_reduce" in names   # before t0, after t1, the max
+        assert el == pytest.approx(max(r[4] for r in res))

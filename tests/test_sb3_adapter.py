@@ -106,6 +106,22 @@ def test_sb3_adapter_semantics_cpu(k):
                 assert abs(infos[i]["episode"]["r"] - ref_infos[i]["episode"]["r"]) < 1e-5
 
 
+def test_sb3_infos_are_fresh_each_step_cpu():
+    """DummyVecEnv returns new info dicts every step: a key a wrapper writes into infos[i] must not
+    reappear in a later step's infos."""
+    fv = FakeVenv(T=10)
+    env = Sb3VecEnv(venv=fv)
+    env.reset()
+    for t in range(10):
+        _, _, _, infos = env.step(np.zeros((fv.num_envs, 2), np.float32))
+        assert len(infos) == fv.num_envs
+        for i, d in enumerate(infos):
+            assert "written_by_wrapper" not in d, (t, i)
+            d["written_by_wrapper"] = t
+        ids = {id(d) for d in infos}
+        assert len(ids) == fv.num_envs                     # no dict shared between envs
+
+
 def test_device_frame_stack_no_final_obs_cpu():
     fs = DeviceFrameStack(3, 2, 3, torch.device("cpu"))
     fs.reset(torch.ones(3, 2))
@@ -155,5 +171,30 @@ def test_sb3_adapter_gpu_matches_raw_env():
             assert infos[i]["episode"]["l"] == ref_infos[i]["episode"]["l"]
             assert abs(infos[i]["episode"]["r"] - ref_infos[i]["episode"]["r"]) < 1e-3
     assert n_done > 0
+    env.close()
+    raw.close()
+
+
+@pytest.mark.gpu
+def test_sb3_adapter_on_non_current_device():
+    """Sb3VecEnv(device=1) while device 0 is current: the copies wait for the step kernel on
+    device 1's stream.  Needs two GPUs; skipped on a one-GPU box."""
+    if torch.cuda.device_count() < 2:
+        pytest.skip("one GPU")
+    import gym_usv_amd
+    n = 256
+    torch.cuda.set_device(0)
+    env = Sb3VecEnv("usv-simple", num_envs=n, seed=5, device=1)
+    raw = gym_usv_amd.make_vec("usv-simple", n, seed=5, device=1)
+    env.reset()
+    raw.reset(seed=5)
+    rng = np.random.default_rng(0)
+    for _ in range(20):
+        a = rng.uniform([0.2, -1], [1, 1], size=(n, 2)).astype(np.float32)
+        o, r, dn, _ = env.step(a)
+        ro, rr, rte, rtr, _ = raw.step(torch.from_numpy(a).to("cuda:1"))
+        np.testing.assert_array_equal(o, ro.cpu().numpy())
+        np.testing.assert_array_equal(r, rr.cpu().numpy())
+        np.testing.assert_array_equal(dn, (rte | rtr).cpu().numpy())
     env.close()
     raw.close()

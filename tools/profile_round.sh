@@ -9,12 +9,13 @@ export TMPDIR=/tmp
 R=${1:-r03}
 ENVS=${ENVS:-65536}
 ENV_ID=${ENV_ID:-usv-simple}
+PREC=${PREC:-f32}
 KERNELS=${KERNELS:-}        # regex of every kernel of a step (usv-asmc-simple: "usv::(step_q_kernel|asmc_chain_kernel)")
 OUT=gpurun_out/prof_$R
 mkdir -p $OUT
 KT_STEPS=${KT_STEPS:-2000}
-B="python3 bench.py --envs $ENVS --env-id $ENV_ID --no-cpu-baseline --api-steps 0"
-P="$B --clock-warmup 0"
+B="python3 bench.py --envs $ENVS --env-id $ENV_ID --precision $PREC --no-cpu-baseline --api-steps 0 --f64-steps 0"
+P="$B --clock-warmup 0 --steady-steps 0"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o kt --output-format csv -- $B --steps $KT_STEPS --warmup 100 > $OUT/kt.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o fetch --output-format csv -- $P --steps 40 --warmup 10 > $OUT/fetch.log 2>&1
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o write --output-format csv -- $P --steps 40 --warmup 10 > $OUT/write.log 2>&1
@@ -28,8 +29,8 @@ cp profiles/pmc_summary.json $OUT/pmc_summary_prev.json 2>/dev/null || true
 mkdir -p $OUT/profiles
 cp profiles/pmc_summary.json $OUT/profiles/pmc_summary.json 2>/dev/null || true
 python3 tools/pmc_summary.py --kt $OUT/kt --fetch $OUT/fetch --write $OUT/write --sq $OUT/sq --envs $ENVS \
-  --key $ENV_ID/$ENVS/f32/window --round $R --out $OUT/profiles ${KERNELS:+--kernels "$KERNELS"}
+  --key $ENV_ID/$ENVS/$PREC/window --round $R --out $OUT/profiles ${KERNELS:+--kernels "$KERNELS"}
 find $OUT/kt -name "*kernel_stats.csv" -exec cp {} $OUT/profiles/${R}_kernel_stats.csv \;
 # bench last, with the default CPU leg at 65 536 envs: it reads roofline.traffic / valu_frac from the summary
-timeout -k 10 300 python bench.py --envs $ENVS --env-id $ENV_ID --pmc $OUT/profiles/pmc_summary.json $([ "$ENVS" != 65536 ] && echo --no-cpu-baseline) > $OUT/bench.json 2> $OUT/bench.err
+timeout -k 10 300 python bench.py --envs $ENVS --env-id $ENV_ID --precision $PREC --pmc $OUT/profiles/pmc_summary.json $([ "$ENVS" != 65536 ] && echo --no-cpu-baseline) > $OUT/bench.json 2> $OUT/bench.err
 tail -1 $OUT/bench.json
