@@ -67,6 +67,8 @@ template <typename R> struct State {
   int N, cap, limit, autoreset;
   int prio;                // scan loops: raise the issue priority of lagging waves (s_setprio)
   int rowspan;             // block-queue step: store an env pair's obs rows as one 32-B-aligned span
+  int qyoung;              // block-queue step: blocks from this index raise kQYoungWaves waves' issue
+                           //   priority (a CU's second block of a one-round grid; INT_MAX: none)
   int fstride;             // elements between fields (>= N, 256-B aligned)
   int ostride;             // obstacle plane stride: cap rounded up to a multiple of 4
   uint64_t seed, gid0;
@@ -176,6 +178,7 @@ template <typename T> __device__ __forceinline__ void st_obs(T* p, T v) {
   st_out(p, v);
 #endif
 }
+
 // Obs-row store layout of the block-queue step (State::rowspan; usv_set_kernel_variant lid bits 0x100 /
 // 0x200 force it on / off; a template switch, SPAN, of the 128-env fused kernels without info rows, as
 // the two layouts' code together in the pair loop spilled SGPRs; the others store pieces): an env pair's two rows as one span of 32-B-aligned 256-B stores (round 4),
@@ -185,6 +188,10 @@ template <typename T> __device__ __forceinline__ void st_obs(T* p, T v) {
 // 256 MB Infinity Cache the pieces are faster (65 536 envs: 19.2 vs 20.3 us), so the default switches
 // at kRowSpanFrom envs.
 constexpr int kRowSpanFrom = 196608;
+#ifndef USV_F64_REC_SOA
+#define USV_F64_REC_SOA 0   // experiment: lidar_wave2_d's per-obstacle records as two 16-B planes
+#endif
+
 // Division and square root of the per-step dynamics: in the f32 build the hardware reciprocal and
 // square root (1 ulp; the reference's float64 values are matched to SURVEY 8(c)'s tolerance), which
 // shortens the dependent chain of the block queue's phase 1 (barrier exit 3.4 -> 2.6 us); IEEE in
@@ -1364,8 +1371,18 @@ __device__ __forceinline__ void lidar_wave2_d(const double* rows, int os, int nl
   // mark: owner lane + 1 in the high bits, slot offset (env B: + 128) in the low bits
   const int mk0 = ((l + 1) << 16) | (lo - off + (l >= 32 ? 128 : 0) + 32768);
   const unsigned long long kq = (ord_key64(key) & ~63ull) | (unsigned long long)l;
+#if USV_F64_REC_SOA
+  // per-obstacle record as two 16-B planes (a, b) [64] and (r^2, key | lane) [64]: lane l's halves at a
+  // 16-B stride, so the stores and the owners' gathers are bank-conflict free (a 32-B record stride
+  // put lanes 4 apart on the same banks)
+  double2* const recA = reinterpret_cast<double2*>(rec);
+  double2* const recB = recA + kWave;
+  recA[l] = make_double2(a, b);
+  recB[l] = make_double2(r2, __longlong_as_double((long long)kq));
+#else
   // per-obstacle record (a, b, r^2, key | lane) in LDS: a pair reads its owner's with two ds_read_b128
   rec[l] = make_double4(a, b, r2, __longlong_as_double((long long)kq));
+#endif
   const int mpass = cnt > 0 ? off >> 6 : -1;
   int carry = 0;
   for (int base = 0, pass = 0; base < W; base += kWave, ++pass) {   // wave-uniform pass count
@@ -1377,7 +1394,12 @@ __device__ __forceinline__ void lidar_wave2_d(const double* rows, int os, int nl
     const int q = base + l;
     const int jj = max((mk >> 16) - 1, 0);
     const int si = (q + (mk & 0xffff) - 32768) & 255;
+#if USV_F64_REC_SOA
+    const double2 oa = recA[jj], ob = recB[jj];
+    const double4 o = make_double4(oa.x, oa.y, ob.x, ob.y);   // owner's (a, b, r^2, key | lane)
+#else
     const double4 o = rec[jj];                         // owner's (a, b, r^2, key | lane)
+#endif
     const unsigned long long jk = (unsigned long long)__double_as_longlong(o.w);
     const double2 cs = rayoff[si & 127];
     const double proj = m_fma(o.x, cs.x, o.y * cs.y);  // ray_pair's arithmetic
@@ -1394,7 +1416,12 @@ __device__ __forceinline__ void lidar_wave2_d(const double* rows, int os, int nl
   mark[l] = 0;
   // reading of the winner (reading_of's arithmetic, the winner's record from LDS)
   auto reading = [&](double c, double sn, unsigned long long v) {
+#if USV_F64_REC_SOA
+    const double2 wa = recA[(int)(v & 63)], wb = recB[(int)(v & 63)];
+    const double4 w = make_double4(wa.x, wa.y, wb.x, wb.y);
+#else
     const double4 w = rec[(int)(v & 63)];
+#endif
     const double proj = m_fma(w.x, c, w.y * sn);
     const double perp = m_fma(w.x, sn, -(w.y * c));
     const double delta = m_fma(-perp, perp, w.z);
@@ -1952,15 +1979,22 @@ void step_kernel_blockdyn(State<R> S, IO<R> io) { step_body_blockdyn<R, MODE, EP
 #ifndef USV_QWPE
 #define USV_QWPE 8       // waves per SIMD it is compiled for
 #endif
+// Issue priority in the block queue (round 5).  VALU issue on a SIMD goes by priority, then age, so a
+// CU's older block (the first one dispatched to it) wins every tie against the younger one: in the
+// round-4 timeline the older block ended at ~11.7 us and the younger ran alone, at 4 waves per SIMD,
+// for its last ~6 us.  (1) The dynamics waves run phase 1 at priority 3 (the younger block's 14 other
+// waves wait at its barrier for them while the older block scans), back to 0 after the barrier;
+// (2) in a one-round grid (<= 2 blocks per CU) the second block of each CU (block index >= the CU
+// count: blocks are dispatched one per CU first) raises kQYoungWaves of its 16 waves to priority 1,
+// so the two blocks progress at more even rates.  A/B on one box (gpurun_out r5b-r5d): -0.27 to
+// -0.44 us per launch at 65 536 envs against the same build without.
 #ifndef USV_QPRIO_DYN
-#define USV_QPRIO_DYN 0  // experiment: issue priority of the dynamics waves in phase 1 (0: default)
+#define USV_QPRIO_DYN 3
 #endif
 #ifndef USV_QPRIO_YOUNG
-#define USV_QPRIO_YOUNG 0  // experiment: second-slot blocks raise waves 0 .. this - 1 to priority USV_QPRIO_YLVL
+#define USV_QPRIO_YOUNG 10
 #endif
-#ifndef USV_QPRIO_YLVL
-#define USV_QPRIO_YLVL 1
-#endif
+constexpr int kQYoungWaves = USV_QPRIO_YOUNG;
 constexpr int kQW = USV_QW, kQE = USV_QE, kQRec = 16;
 __host__ __device__ constexpr size_t q_slice_bytes() { return 256 * 8 + 64 * 4 + 2 * 1024; }
 
@@ -2088,6 +2122,7 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
     qdyn[0] = 0u;
     qdyn[1] = 0u;
   }
+
   // the ray table: by the last wave, so that the dynamics waves (fused) issue no DMA of their own
   if (wave == kQW - 1) dma_copy(S.ray_tab, lds, (int)wave_tab_bytes<float>());
 #pragma unroll
@@ -2147,9 +2182,7 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
 #if USV_QPRIO_DYN
   if (FUSED && wave < kDynWaves) __builtin_amdgcn_s_setprio(0);
 #endif
-#if USV_QPRIO_YOUNG
-  if (2 * blockIdx.x >= gridDim.x && wave < USV_QPRIO_YOUNG) __builtin_amdgcn_s_setprio(USV_QPRIO_YLVL);
-#endif
+  if ((int)blockIdx.x >= S.qyoung && wave < kQYoungWaves) __builtin_amdgcn_s_setprio(1);
   USV_STAMP_W(2);
   QMARK(0);
   unsigned tk = 0;
@@ -2160,6 +2193,7 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
   const bool hb = l >= 32;
   auto pair_hasb = [&](int p) { return 2 * p + 1 < nbe; };
   const float* const oblk = S.orow(eb);               // this block's obstacle rows (pair p at 2 p rowb bytes)
+
   // An env pair's two obs rows are one 1144-B span, stored as five 256-B wave stores from the span's
   // first 32-B sector: every sector but the two at the span's ends is written whole by one write-through
   // store (the four sensor halves and the header store of round 3 split ~3 sectors per row between
@@ -2264,6 +2298,7 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
       } else {
         // per-row pieces: each row's sensors in two 256-B stores and the two headers in one (a lone
         // env, odd env count: env A's row twice, identical values to identical addresses)
+        {
         float* const rowB = rowA + (hasB ? kObsDim : 0);
         st_obs(rowA + kHdr + l, l_norm(sa.rd0));
         st_obs(rowA + kHdr + 64 + l, l_norm(sa.rd1));
@@ -2277,6 +2312,7 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
           const bool hB = ((hpk >> 16) & 1) && hasB;    // (no env B: env A's value again)
           const float hc = hi == 12 ? (float)(kMaxAccU / 10.0) : hi == 14 ? (float)(kMaxAccR / 10.0) : 0.0f;
           st_obs(rowA + (hB ? kObsDim : 0) + hi, ((hpk >> 17) & 1) ? hc : hv);
+        }
         }
       }
       const bool term_l = hb ? termB : sa.term;         // reward, terminated: lanes 0..31 env A,
@@ -2853,6 +2889,7 @@ struct Handle {
   //   4 / 5 = block-queue step, split / fused (step_q_kernel; f32 window lidar, cap <= 32)
   int epb = 64, lid = 7, kind = 1;
   int prio = 1;                        // scan loops raise the priority of lagging waves
+  int cus = 256;                       // compute units of the device (State::qyoung)
   void* slab = nullptr;
   void* exp_buf = nullptr;             // device usv_experiment record (kExp* layout, in R)
   State<float> sf{};
@@ -2910,6 +2947,7 @@ int carve(Handle* h, State<R>& S) {
   S.autoreset = h->cfg.autoreset;
   S.prio = h->prio;
   S.rowspan = h->cfg.num_envs >= kRowSpanFrom;
+  S.qyoung = INT_MAX;                                    // (set per launch: launch_step)
   S.seed = h->cfg.seed;
   S.gid0 = h->cfg.env_id_offset;
   // ray offsets start + i*res (usv_asmc_ca_env.py:420), cos/sin in float64 on the host
@@ -3056,6 +3094,9 @@ int launch_step_kernels(Handle* h, State<R>& S, const float* act, float* obs, vo
         HIP_TRY(hipLaunchKernel((void*)&asmc_chain_kernel<float>, dim3((S.N + kBlock - 1) / kBlock), dim3(kBlock), args, 0, st));
       const bool small = h->kind != 4 && h->epb == kQE_S;
       const int qe = small ? kQE_S : kQE, qw = small ? kQW_S : kQW;
+      // a one-round grid of the 128-env blocks: the second block of each CU raises priority
+      const int nblk = (S.N + qe - 1) / qe;
+      S.qyoung = (!small && nblk > h->cus && nblk <= 2 * h->cus) ? h->cus : INT_MAX;
       HIP_TRY(hipLaunchKernel(pick_q(h->cfg.mode, h->kind != 4, small, io.done != nullptr, h->kind == 6,
                                      io.info != nullptr, S.rowspan != 0),
                               dim3((S.N + qe - 1) / qe), dim3(qw * kWave), args,
@@ -3431,6 +3472,11 @@ int usv_create(const usv_config* cfg, int32_t device, void** out) {
   Handle* h = new Handle();
   h->cfg = *cfg;
   h->device = device;
+  {
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && cus > 0)
+      h->cus = cus;
+  }
   h->lid = cfg->lidar_algo == USV_LIDAR_BRUTE ? (kLidSkip | kLidUnroll2) : (kLidSkip | kLidUnroll2 | kLidWindow);
   // tuned defaults at 65 536 envs on MI355X (tools/sweep_variants.py, profiles/): usv-simple
   // (f32, window lidar) runs the fused block-queue step, else the fused wave kernel at 16

@@ -10,6 +10,7 @@ observation in ``info["final_obs"]``), and the TimeLimit of the registered id
 from __future__ import annotations
 
 import ctypes
+import sys
 import warnings
 
 import numpy as np
@@ -275,15 +276,9 @@ class UsvVectorEnv:
         if a.shape != (self.num_envs, self.act_dim):
             raise ValueError(f"actions must be [{self.num_envs}, {self.act_dim}], got {tuple(a.shape)}")
         if self.copy:
-            # fresh outputs: the kernel writes every row of obs / reward / flags (and of the info rows),
-            # so new tensors cost an allocation, not a copy
-            n, dev = self.num_envs, self.device
-            obs = torch.empty((n, self.obs_dim), dtype=torch.float32, device=dev)
-            fobs = torch.empty((n, self.obs_dim), dtype=torch.float32, device=dev)
-            rew = torch.empty(n, dtype=self._rdt, device=dev)
-            term, trunc, done = torch.empty((3, n), dtype=torch.bool, device=dev).unbind(0)
-            ib = torch.empty_like(self.info_buf) if self.info_enabled else None
-            ptrs = (_ptr(obs), _ptr(rew), _ptr(term), _ptr(trunc), _ptr(done), _ptr(fobs), _ptr(ib))
+            # fresh outputs: tensors no one else references (the kernel writes every row of obs /
+            # reward / flags and of the info rows, so they need no copy)
+            (obs, rew, term, trunc, done, fobs, ib), ptrs = self._fresh_outputs()
         else:
             obs, rew, fobs, ib = self.obs, self.reward, self.final_obs, self.info_buf
             term, trunc, done = self._term_b, self._trunc_b, self._done_b
@@ -298,6 +293,47 @@ class UsvVectorEnv:
             self.info_buf = ib
             info.update(self._info_dict(ib, rew))
         return obs, rew, term, trunc, info
+
+    _RING = 3
+
+    def _fresh_outputs(self):
+        """One output set of a copy=True step: (obs, reward, terminated, truncated, done, final_obs,
+        info rows) and their ctypes pointers.  A set is one device allocation viewed as the outputs;
+        a set returned earlier is handed out again only when nothing outside this env refers to it
+        any more -- none of its tensor objects is referenced elsewhere and its storage has no other
+        view -- so the caller always gets tensors that alias nothing it holds (gymnasium's copy=True),
+        at the cost of two reference-count reads instead of five caching-allocator calls per step.
+        Work queued on other streams that reads a dropped output must record that stream on it, as
+        for any tensor the caching allocator may reuse."""
+        ring = self.__dict__.setdefault("_out_ring", [])
+        for ent in ring:
+            ts, st, base_use, ptrs = ent
+            if sys.getrefcount(ts) <= 3 and all(sys.getrefcount(t) <= 3 for t in ts if t is not None) and \
+                    torch._C._storage_Use_Count(st._cdata) == base_use:
+                return ts, ptrs
+        n, d, dev = self.num_envs, self.obs_dim, self.device
+        rb = torch.empty((), dtype=self._rdt).element_size()
+        ob = n * d * 4
+        info_b = n * _lib.INFO_DIM * rb if self.info_enabled else 0
+        # byte layout: rewards and info rows first (8-B aligned), then obs, final obs, the flags
+        sizes = (n * rb, info_b, ob, ob, 3 * n)
+        buf = torch.empty(sum(sizes), dtype=torch.uint8, device=dev)
+        rew_b, info_bytes, obs_b, fobs_b, flags = buf.split(sizes)
+        rew = rew_b.view(self._rdt)
+        ib = info_bytes.view(self._rdt).view(n, _lib.INFO_DIM) if self.info_enabled else None
+        obs = obs_b.view(torch.float32).view(n, d)
+        fobs = fobs_b.view(torch.float32).view(n, d)
+        term, trunc, done = flags.view(torch.bool).view(3, n).unbind(0)
+        ts = (obs, rew, term, trunc, done, fobs, ib)
+        del rew_b, info_bytes, obs_b, fobs_b, flags
+        st = buf.untyped_storage()
+        del buf
+        base_use = torch._C._storage_Use_Count(st._cdata)
+        ptrs = (_ptr(obs), _ptr(rew), _ptr(term), _ptr(trunc), _ptr(done), _ptr(fobs), _ptr(ib))
+        if len(ring) >= self._RING:
+            ring.pop(0)                                # (still the caller's if it holds it)
+        ring.append((ts, st, base_use, ptrs))
+        return ts, ptrs
 
     def step_raw(self, actions, obs, reward, term, trunc, final_obs=None, stream=None):
         """Launch one step into caller-owned buffers (no checks, no allocation): bench / graphs."""

@@ -443,7 +443,7 @@ def _f32(x):
     return np.asarray(x, dtype=np.float32).astype(np.float64)
 
 
-def gen_asmc_highspeed(E, fname="asmc_highspeed.npz", n_env=48, T=8):
+def gen_asmc_highspeed(E, fname="asmc_highspeed.npz", n_env=48, T=8, seed=4040, seed0=8000):
     """usv-asmc-simple steps (simple_env_asmc.py:18-27) from harness-injected states outside the
     low-speed regime the action space reaches: u in [-1, 4] (UsvAsmc's |u| > 1.2 hydrodynamics,
     usv_asmc.py:95-99), r in [-1, 1], v in [-0.1, 0.1] (the reference's explicit integrator diverges
@@ -462,9 +462,9 @@ def gen_asmc_highspeed(E, fname="asmc_highspeed.npz", n_env=48, T=8):
                 self.position, self.velocity, _ = self.asmc.compute(action, self.position, self.velocity, True)
             return E.UsvSimpleEnv.step(self, np.zeros(2))
 
-    rng = np.random.default_rng(4040)
+    rng = np.random.default_rng(seed)
     perturb = (np.arange(n_env) % 2) == 1
-    seeds = np.arange(n_env) + 8000
+    seeds = np.arange(n_env) + seed0
     acts = np.zeros((n_env, T, 2), np.float32)
     acts[:, :, 0] = np.where(rng.uniform(size=(n_env, T)) < 0.6, rng.uniform(0.2, 10, (n_env, T)),
                              rng.uniform(0.2, 1, (n_env, T)))
@@ -522,6 +522,9 @@ def gen_asmc_highspeed(E, fname="asmc_highspeed.npz", n_env=48, T=8):
 def main():
     refharness.load_reference()
     import gym_usv.envs as E
+    if "--r5" in sys.argv:              # round-5 fixture only: the high-speed generator at 240 envs
+        gen_asmc_highspeed(E, fname="asmc_highspeed_240.npz", n_env=240, seed=4041, seed0=9000)
+        return
     if "--r4" in sys.argv:              # round-4 fixtures only (existing files untouched)
         gen_asmc_highspeed(E)
         return

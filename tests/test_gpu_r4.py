@@ -36,19 +36,29 @@ def to_np(*ts):
 # velocity 2.5e-16, ASMC state 1.8e-13 (OCML's exp / asin / sin / cos against glibc's differ in the last
 # bit, and 20 substeps carry it); f32: header 7.1e-6 (8(c) 1e-5), reward 3.5e-5 (8(c) 1e-4), pose /
 # velocity 3.5e-5 relative, state 1.6e-3.
-HS_TOL = {"f64": dict(hdr=0.0, rew=2e-14, vel=2e-15, state=1e-12),
-          "f32": dict(hdr=1e-5, rew=1e-4, vel=1.5e-4, state=5e-3)}
+# Round 5 (240-env fixture, 5x more envs): f64 reward 4.0e-14, state 6.2e-13; f32 state 7.4e-3 (row 7,
+# the surge acceleration u_dot_last, relative to max(1, |ref|)) -- bounds raised to ~5x / ~3x those.
+HS_TOL = {"f64": dict(hdr=0.0, rew=2e-13, vel=2e-15, state=3e-12),
+          "f32": dict(hdr=1e-5, rew=1e-4, vel=1.5e-4, state=2.5e-2)}
 
 
+# f32 envs whose Ka switch lands on the other branch (the round-5 240-env fixture gives the rate
+# statistical weight): bound = 2x the measured count per fixture and mode (round 5: 48-env fixture
+# 1/24 plain, 0/24 perturbed; 240-env fixture 4/120 plain, 3/120 perturbed, i.e. 2.5-3.3 %)
+HS_FLIPS = {("asmc_highspeed.npz", False): 2, ("asmc_highspeed.npz", True): 1,
+            ("asmc_highspeed_240.npz", False): 8, ("asmc_highspeed_240.npz", True): 6}
+
+
+@pytest.mark.parametrize("fixture", ["asmc_highspeed.npz", "asmc_highspeed_240.npz"], ids=["48", "240"])
 @pytest.mark.parametrize("precision", ["f64", "f32"])
 @pytest.mark.parametrize("perturb", [False, True], ids=["plain", "perturb"])
-def test_asmc_highspeed_replay(golden, precision, perturb):
+def test_asmc_highspeed_replay(golden, precision, perturb, fixture):
     """Up to each env's first episode end.  The adaptive-gain derivatives Ka_dot_u / Ka_dot_psi
     (usv_asmc.py:137-140) are switches (+-k, k_min): in f32 a sliding surface within rounding of
     its threshold mu picks the other branch, after which that env follows another control law.
     Such envs are counted (a branch-flip rate, bounded) and compared no further; the others
     are held to the stated bounds."""
-    g = golden("asmc_highspeed.npz")
+    g = golden(fixture)
     idx = np.flatnonzero(g["perturb"] == perturb)
     n, T = len(idx), g["actions"].shape[1]
     env = make("usv-asmc-simple", n, precision=precision, autoreset=False, info=True, perturb=perturb)
@@ -58,6 +68,7 @@ def test_asmc_highspeed_replay(golden, precision, perturb):
     flipped = np.zeros(n, bool)
     worst = dict(hdr=0.0, rew=0.0, vel=0.0, pos=0.0, state=0.0)
     flips = rays = 0
+    worst_entry = -1
     cont = np.array([k for k in range(16) if k not in (11, 12)])    # continuous state entries
     band = idx % 3                              # gen_asmc_highspeed: |psi| <= pi, <= 30, 300..400 rad
     bw = {b: dict(hdr=0.0, rew=0.0, flips=0) for b in range(3)}
@@ -80,7 +91,9 @@ def test_asmc_highspeed_replay(golden, precision, perturb):
             worst["vel"] = max(worst["vel"], float((np.abs(ivel[m] - rv) / np.maximum(1, np.abs(rv))).max()))
             worst["pos"] = max(worst["pos"], float((np.abs(ipos[m] - rp) / np.maximum(1, np.abs(rp))).max()))
             d = np.abs(st[m][:, cont] - rs[m][:, cont]) / np.maximum(1, np.abs(rs[m][:, cont]))
-            worst["state"] = max(worst["state"], float(d.max()))
+            if float(d.max()) > worst["state"]:
+                worst["state"] = float(d.max())
+                worst_entry = int(cont[np.unravel_index(np.argmax(d), d.shape)[1]])
             for b in range(3):
                 mb = m & (band == b)
                 if mb.any():
@@ -92,12 +105,14 @@ def test_asmc_highspeed_replay(golden, precision, perturb):
             np.testing.assert_array_equal(trunc[m], g["truncated"][idx][m, t], err_msg=f"t={t}")
         alive &= ~(g["terminated"][idx][:, t] | g["truncated"][idx][:, t])
     fast = int(orc.asmc.fast_substeps.sum())
-    print(f"\n[asmc highspeed {precision} perturb={perturb}] {fast} substeps with |u| > 1.2 over {n} envs; "
-          f"Ka-switch flips {int(flipped.sum())}/{n} envs; "
-          + ", ".join(f"{k} {v:.2e}" for k, v in worst.items()) + f"; sensor flips {flips}/{rays}; by |psi| band "
+    print(f"\n[asmc highspeed {fixture} {precision} perturb={perturb}] {fast} substeps with |u| > 1.2 over {n} envs; "
+          f"Ka-switch flips {int(flipped.sum())}/{n} envs (rate {flipped.mean():.3f}); "
+          + ", ".join(f"{k} {v:.2e}" for k, v in worst.items()) + f" (state row {worst_entry})"
+          + f"; sensor flips {flips}/{rays}; by |psi| band "
           + "; ".join(f"{b}: hdr {v['hdr']:.2e} rew {v['rew']:.2e} flips {v['flips']}" for b, v in bw.items()))
     assert fast > 0 and (orc.asmc.fast_substeps > 0).sum() >= n // 3
-    assert flipped.sum() <= (0 if precision == "f64" else max(2, n // 8)), flipped.sum()
+    assert flipped.sum() <= (0 if precision == "f64" else HS_FLIPS.get((fixture, perturb), max(2, n // 8))), \
+        flipped.sum()
     tol = HS_TOL[precision]
     assert worst["hdr"] <= tol["hdr"] and worst["rew"] <= tol["rew"], worst
     assert worst["vel"] <= tol["vel"] and worst["pos"] <= tol["vel"] and worst["state"] <= tol["state"], worst
@@ -106,6 +121,13 @@ def test_asmc_highspeed_replay(golden, precision, perturb):
 
 
 # --------------------------------------------------------------------------- the controller on its own
+# calls 350..1000 of the reference KATs (round 5; measured in parentheses): kat_fwd stays smooth
+# (f64 5.2e-15, f32 1.9e-5); kat_rot's heading-rate switching makes even f64 drift (9.3e-2 on psi,
+# u, r at call 1000), f32 8.6e-2 -- a band around the reference trajectory, not a tolerance
+KAT_BAND = {"f64": {"kat_zero": 0.0, "kat_fwd": 3e-14, "kat_rot": 0.2},
+            "f32": {"kat_zero": 0.0, "kat_fwd": 1e-4, "kat_rot": 0.25}}
+
+
 @pytest.mark.parametrize("precision", ["f64", "f32"])
 def test_reference_asmc_tests_on_hip(golden, precision):
     """The reference's own tests (tests/test_usv_asmc.py:8-37: 1000 compute() calls from rest),
@@ -115,6 +137,7 @@ def test_reference_asmc_tests_on_hip(golden, precision):
     from gym_usv_amd.control import UsvAsmc
     g = golden("asmc_compute.npz")
     worst = 0.0
+    band = {}
     for name, act in (("kat_zero", [0, 0]), ("kat_fwd", [10, 0]), ("kat_rot", [0, 10])):
         asmc = UsvAsmc(precision=precision)
         position, velocity = np.zeros(3), np.zeros(3)
@@ -134,10 +157,21 @@ def test_reference_asmc_tests_on_hip(golden, precision):
         ref = g[name]
         err = np.abs(traj[:55] - ref[:55]) / np.maximum(1, np.abs(ref[:55]))
         worst = max(worst, float(err.max()))
+        # calls 350..1000 (round 5): a property band, since sign() switches amplify last-bit
+        # differences there (f64 too).  kat_fwd stays smooth: relative error on every entry;
+        # kat_rot: surge speed u, yaw rate r and heading psi (x, y wander around 0 and are bounded
+        # by the reference test itself)
+        late = np.abs(traj[55:] - ref[55:]) / np.maximum(1, np.abs(ref[55:]))
+        if name == "kat_rot":
+            late = late[:, [2, 3, 5]]
+        band[name] = float(late.max())
         print(f"\n[KAT {name} {precision}] final pos {position}, vel {velocity}; ref final {ref[-1]}; "
-              f"first 300 calls max rel err {err.max():.2e}")
+              f"first 300 calls max rel err {err.max():.2e}; calls 350-1000 band {band[name]:.2e}")
     # measured: f64 5.7e-15, f32 4.4e-5 (kat_rot)
     assert worst <= (3e-14 if precision == "f64" else 2.5e-4), worst
+    # calls 350-1000, measured (round 5): see KAT_BAND
+    for name, lim in KAT_BAND[precision].items():
+        assert band[name] <= lim, (name, band[name])
 
 
 @pytest.mark.parametrize("precision", ["f64", "f32"])

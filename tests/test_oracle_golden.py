@@ -266,13 +266,14 @@ def test_asmc_simple_step_info_matches_reference(golden):
 
 
 # --------------------------------------------------------------------------- round-4 fixtures
+@pytest.mark.parametrize("fixture", ["asmc_highspeed.npz", "asmc_highspeed_240.npz"], ids=["48", "240"])
 @pytest.mark.parametrize("perturb", [False, True], ids=["plain", "perturb"])
-def test_asmc_highspeed_steps_match_reference(golden, perturb):
+def test_asmc_highspeed_steps_match_reference(golden, perturb, fixture):
     """usv-asmc-simple from injected states outside the action space's low-speed regime
     (make_golden.py gen_asmc_highspeed): |u| > 1.2 hydrodynamics (usv_asmc.py:95-99), headings to
     400 rad, adaptive gains to 5, u_d to 10; with and without do_perturb (:184-199)."""
     from asmc_fixture import asmc_state, oracle_env
-    g = golden("asmc_highspeed.npz")
+    g = golden(fixture)
     idx = np.flatnonzero(g["perturb"] == perturb)
     e = oracle_env(g, idx, perturb)
     elapsed = g["inj_elapsed"][idx].copy()

@@ -198,3 +198,48 @@ def test_sb3_adapter_on_non_current_device():
         np.testing.assert_array_equal(dn, (rte | rtr).cpu().numpy())
     env.close()
     raw.close()
+
+
+def test_copy_outputs_are_reused_only_when_unreferenced_cpu():
+    """UsvVectorEnv's copy=True output sets (vector_env._fresh_outputs): a set comes back only once
+    nothing outside the env refers to any of its tensors or to a view of them."""
+    from gym_usv_amd import _lib
+    from gym_usv_amd.vector_env import UsvVectorEnv
+
+    class Fake:
+        _RING = UsvVectorEnv._RING
+        _fresh_outputs = UsvVectorEnv._fresh_outputs
+
+        def __init__(self):
+            self.num_envs, self.obs_dim, self.device = 8, 143, torch.device("cpu")
+            self._rdt, self.info_enabled = torch.float32, True
+
+    f = Fake()
+    a, _ = f._fresh_outputs()
+    assert a[0].shape == (8, 143) and a[1].shape == (8,) and a[2].dtype == torch.bool
+    assert a[6].shape == (8, _lib.INFO_DIM)
+    ptr_a = a[0].data_ptr()
+    b, _ = f._fresh_outputs()                  # `a` is held: a new set
+    assert b[0].data_ptr() != ptr_a
+    del a, b
+    c, _ = f._fresh_outputs()                  # nothing held: the first set again
+    assert c[0].data_ptr() == ptr_a
+    view = c[0][:, :15]                        # only a view of one output is kept
+    del c
+    d, _ = f._fresh_outputs()
+    assert d[0].data_ptr() != ptr_a
+    held = d[4]                                # the done mask alone
+    ptr_d = d[0].data_ptr()
+    del d
+    e, _ = f._fresh_outputs()
+    assert e[0].data_ptr() not in (ptr_a, ptr_d)
+    assert len(f._out_ring) <= UsvVectorEnv._RING
+    del view, held, e
+    obs, rew, *_ = f._fresh_outputs()[0]       # as step() hands them out: one tensor kept
+    p_obs = obs.data_ptr()
+    del _
+    nxt = f._fresh_outputs()[0]
+    assert nxt[0].data_ptr() != p_obs
+    del nxt, rew
+    assert f._fresh_outputs()[0][0].data_ptr() != p_obs    # obs still held
+    del obs
