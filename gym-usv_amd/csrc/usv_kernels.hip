@@ -188,8 +188,11 @@ template <typename T> __device__ __forceinline__ void st_obs(T* p, T v) {
 // 256 MB Infinity Cache the pieces are faster (65 536 envs: 19.2 vs 20.3 us), so the default switches
 // at kRowSpanFrom envs.
 constexpr int kRowSpanFrom = 196608;
+#ifndef USV_QFLAG
+#define USV_QFLAG 3   // block queue: same-step resets wait for the dynamics waves' store flag (0: diagnostic off)
+#endif
 #ifndef USV_F64_REC_SOA
-#define USV_F64_REC_SOA 0   // experiment: lidar_wave2_d's per-obstacle records as two 16-B planes
+#define USV_F64_REC_SOA 1   // lidar_wave2_d's per-obstacle records as two 16-B planes (round 5; 0: one 32-B record)
 #endif
 
 // Division and square root of the per-step dynamics: in the f32 build the hardware reciprocal and
@@ -690,13 +693,18 @@ __device__ void env_dynamics(const State<R>& S, int e, float a_u, float a_r, flo
     k0 = S.I(I_TURNS)[e];
     if constexpr (kAsmc && !CHAIN) pdl = S.asmc[e];
   }
+  // every load of the step before its first store (the state stores go out early, below): with one
+  // in-order vmcnt counter a load issued after a store returns only once that store is acknowledged
+  const R lu = S.F(F_LAST_U)[e], lr = S.F(F_LAST_R)[e];
+  const R mu = S.F(F_MAX_U)[e], mr = S.F(F_MAX_R)[e], refv = S.F(F_REF_V)[e];
+  const R x0 = S.F(F_PX0)[e], y0 = S.F(F_PY0)[e];
+  const R x1 = S.F(F_PX1)[e], y1 = S.F(F_PY1)[e];
+  const R prog0 = S.F(F_PROGRESS)[e];
   if (kAsmc) {
     if constexpr (CHAIN) asmc_env_chain<R>(S, e, el0, a_u, a_r, x, y, psi, u, v, r, kF32 ? &pdl : nullptr);
     a_u = 0.0f;                                                                   // step(zeros(2))
     a_r = 0.0f;
   }
-  const R lu = S.F(F_LAST_U)[e], lr = S.F(F_LAST_R)[e];
-  const R mu = S.F(F_MAX_U)[e], mr = S.F(F_MAX_R)[e], refv = S.F(F_REF_V)[e];
   // action = max_action * insert(action, 1, 0); filtered 0.8/0.2 (:311-317)
   const R a3u = R(0.8) * lu + R(0.2) * (mu * R(a_u));
   const R a3r = R(0.8) * lr + R(0.2) * (mr * R(a_r));
@@ -712,12 +720,32 @@ __device__ void env_dynamics(const State<R>& S, int e, float a_u, float a_r, flo
   y = y + (u * sp) * R(kDt);
   psi = psi + r * R(kDt);
   // _get_closest_point (:139-148)
-  const R x0 = S.F(F_PX0)[e], y0 = S.F(F_PY0)[e];
-  const R dx = S.F(F_PX1)[e] - x0, dy = S.F(F_PY1)[e] - y0;
+  const R dx = x1 - x0, dy = y1 - y0;
   const R det = dx * dx + dy * dy;
   R a = dyn_div(dy * (y - y0) + dx * (x - x0), det);
   a = a + R(kLookahead);
-  a = m_clip(a, S.F(F_PROGRESS)[e], R(1));
+  a = m_clip(a, prog0, R(1));
+  const int el = el0 + 1;
+  // the state stores, as soon as the new state exists (their acknowledgements then overlap the rest
+  // of phase 1; a same-step reset by another wave orders itself after them: step_q_body)
+  {
+    R ps = psi;
+    if constexpr (kF32) {                            // the rebase (see the heading representation)
+      // branch-free and stored unconditionally (n = 0 leaves both values unchanged, bit for bit): a
+      // conditional store made the compiler sink the k0 load into its branch, and a wave with one
+      // rebasing lane then waited a memory round trip in the middle of phase 1
+      const float n = turns_of(psi);
+      ps = sub_turns(psi, n);
+      S.I(I_TURNS)[e] = k0 + (int)n;
+      if constexpr (kAsmc) S.asmc[e] = sub_turns(pdl, n);   // (the chain left row 0 to this store)
+    }
+    S.F(F_X)[e] = x; S.F(F_Y)[e] = y; S.F(F_PSI)[e] = ps;
+    S.F(F_U)[e] = u; S.F(F_V)[e] = v; S.F(F_R)[e] = r;
+    S.F(F_LAST_U)[e] = a3u; S.F(F_LAST_R)[e] = a3r;
+    S.F(F_PROGRESS)[e] = a;
+    S.I(I_ELAPSED)[e] = el;
+    S.I(I_SCAN)[e] = 1;
+  }
   const R tx = x0 + a * dx, ty = y0 + a * dy;
   // _get_ye (:133-137): sin/cos of the path angle a_k = atan2(dy, dx) are dy/|d|, dx/|d|
   const R inv_len = dyn_div(R(1), dyn_sqrt(det));
@@ -727,7 +755,6 @@ __device__ void env_dynamics(const State<R>& S, int e, float a_u, float a_r, flo
   const R angle = wrap_angle(fx_atan2(ty - y, tx - x) - psi);
   const R ddx = x - tx, ddy = y - ty;
   const R dist = dyn_sqrt(ddx * ddx + ddy * ddy);
-  const int el = el0 + 1;
   trunc = (x > R(kBound)) | (x < R(0)) | (y > R(kBound)) | (y < R(0)) |   // :336
           (S.limit > 0 && el >= S.limit);                                 // TimeLimit
   make_header<R>(hdr, u, v, r, angle, dist, ye, refv, lu, lr, mu, mr);   // obs uses PREVIOUS action
@@ -742,28 +769,13 @@ __device__ void env_dynamics(const State<R>& S, int e, float a_u, float a_r, flo
   partial = ye_r + ang_r + vel_r + dact_r;
   if (info) {                                        // _get_info + reward_info (:102-115, :189-199)
     const R vals[USV_INFO_DIM] = {x, y, heading_abs(psi, k0), u, v, r,
-                                  x0, y0, S.F(F_PX1)[e], S.F(F_PY1)[e], a3u, a3r, ye,
+                                  x0, y0, x1, y1, a3u, a3r, ye,
                                   cdiv(angle, kPi), ye_r, ang_r, dact_r, dact, vel_r, refv, lu, lu - refv};
 #pragma unroll
     for (int i = 0; i < USV_INFO_DIM; ++i) info[i] = vals[i];
   }
   px = x; py = y;
   heading_sincos(psi, &psp, &pcp);
-  if constexpr (kF32) {                              // the rebase (see the heading representation)
-    // branch-free and stored unconditionally (n = 0 leaves both values unchanged, bit for bit): a
-    // conditional store made the compiler sink the k0 load into its branch, and a wave with one
-    // rebasing lane then waited a memory round trip in the middle of phase 1
-    const float n = turns_of(psi);
-    psi = sub_turns(psi, n);
-    S.I(I_TURNS)[e] = k0 + (int)n;
-    if constexpr (kAsmc) S.asmc[e] = sub_turns(pdl, n);   // (the chain left row 0 to this store)
-  }
-  S.F(F_X)[e] = x; S.F(F_Y)[e] = y; S.F(F_PSI)[e] = psi;
-  S.F(F_U)[e] = u; S.F(F_V)[e] = v; S.F(F_R)[e] = r;
-  S.F(F_LAST_U)[e] = a3u; S.F(F_LAST_R)[e] = a3r;
-  S.F(F_PROGRESS)[e] = a;
-  S.I(I_ELAPSED)[e] = el;
-  S.I(I_SCAN)[e] = 1;
 }
 
 // --------------------------------------------------------------------------- lidar
@@ -1624,12 +1636,10 @@ __device__ __forceinline__ void emit_env(const State<R>& S, const IO<R>& io, int
 // P = (x, y, sin psi, cos psi), obstacle count nl, truncation bits trunc_m.  Writes the sensor
 // half of each obs row, final obs and stale scan of done envs; returns term / collision bits.
 // Precondition: the prologue DMAs have landed and the ray table is published.
-// sig (kind 3, wave 0): set to 1 once every memory op issued before the scan (the block's dynamics
-// stores) is complete.
 template <typename R, int MODE, int LID>
 __device__ __forceinline__ void scan_envs(const State<R>& S, const IO<R>& io, const ScanLds<R>& L, int e0,
                                           int ne, const R4<R>& P, int nl, unsigned trunc_m,
-                                          unsigned& term_m, unsigned& coll_m, Prof& prof, unsigned* sig = nullptr) {
+                                          unsigned& term_m, unsigned& coll_m, Prof& prof) {
   const int cap = S.cap;
   const int rowb = row_bytes<R>(cap);
   const int step = scan_step<R, LID>(cap);
@@ -1647,7 +1657,6 @@ __device__ __forceinline__ void scan_envs(const State<R>& S, const IO<R>& io, co
     // sensor-row stores after their DMA (a full pair: four), so all older ops are done
     if (k > 0) {
       if (step == 2) vm_wait<4>(); else vm_wait<2>();
-      if (sig && k == step) *sig = 1u;
     }
     if (k + step < ne)
       dma_copy(S.orow(e0 + k + step), ((k / step) & 1) ? L.row0 : L.row1, min(step, ne - k - step) * rowb);
@@ -1703,20 +1712,14 @@ __device__ __forceinline__ void scan_envs(const State<R>& S, const IO<R>& io, co
     emit(k, sc);
     prof.mark(3);
   }
-  if (sig && ne <= step) {                         // (one iteration: no wait above)
-    vm_wait<0>();
-    *sig = 1u;
-  }
 }
 
 // Epilogue shared by both: terminated flag and collision term of the reward (lane-per-env),
 // then same-step autoreset of the done envs.
-// dynsig (kind 3): the flag scan_envs(sig) sets on the wave that ran this env's dynamics; a reset
-// waits for it, so the dynamics' state stores cannot land after the reset's.
 template <typename R, int MODE>
 __device__ __forceinline__ void scan_epilogue(const State<R>& S, const IO<R>& io, int e0, int ne,
                                               R partial, bool have_partial, unsigned term_m,
-                                              unsigned coll_m, unsigned trunc_m, const unsigned* dynsig = nullptr) {
+                                              unsigned coll_m, unsigned trunc_m) {
   const int l = lane_id();
   if (l < ne) {
     const int e = e0 + l;
@@ -1728,9 +1731,6 @@ __device__ __forceinline__ void scan_epilogue(const State<R>& S, const IO<R>& io
     if (io.done) io.done[e] = ((term_m | trunc_m) >> l) & 1;
   }
   if (S.autoreset == USV_AUTORESET_SAME_STEP) {
-    if (dynsig && (term_m | trunc_m))
-      while (__hip_atomic_load(dynsig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
-        __builtin_amdgcn_s_sleep(2);
     for (int k = 0; k < ne; ++k)
       if (((term_m | trunc_m) >> k) & 1) reset_wave<R, MODE>(S, e0 + k, io.obs + (size_t)(e0 + k) * kObsDim);
   }
@@ -1875,7 +1875,7 @@ void scan_kernel_d(State<R> S, IO<R> io) { scan_body<R, MODE, EPW, LID, WPB>(S, 
 // flight.  Same per-env arithmetic as kinds 1 and 2, one launch instead of two (no pose records
 // through HBM, no second launch ramp).
 template <typename R> __host__ __device__ constexpr size_t lds_blockdyn_bytes(int cap) {
-  return (lds_scan_bytes<R>(cap) + 31) / 32 * 32 + 2 * kWave * sizeof(R4<R>) + 16;   // + wave 0's store flag
+  return (lds_scan_bytes<R>(cap) + 31) / 32 * 32 + 2 * kWave * sizeof(R4<R>);
 }
 template <typename R, int MODE, int EPW, int LID>
 __device__ __forceinline__ void step_body_blockdyn(const State<R>& S, const IO<R>& io) {
@@ -1889,8 +1889,6 @@ __device__ __forceinline__ void step_body_blockdyn(const State<R>& S, const IO<R
   const int ne = min(EPW, S.N - e0);
   const ScanLds<R> L = scan_lds<R>(lds, wave, S.cap);
   R4<R>* const rec = reinterpret_cast<R4<R>*>(lds + (lds_scan_bytes<R>(S.cap) + 31) / 32 * 32);
-  unsigned* const dynsig = reinterpret_cast<unsigned*>(rec + 2 * kWave);   // wave 0's stores complete
-  if (threadIdx.x == 0) *dynsig = 0u;
   Prof prof;
   USV_STAMP_W(0);
   USV_STAMP_ID();
@@ -1913,9 +1911,11 @@ __device__ __forceinline__ void step_body_blockdyn(const State<R>& S, const IO<R
     rec[l] = R4<R>{px, py, sp, cp};
     rec[kWave + l] = R4<R>{partial, R(nob), R(trunc ? 1 : 0), R(0)};
     USV_STAMP_W(1);
-    if (io.fobs) {
-      // waves 1-3 read these header rows back for their done envs' terminal obs (emit_env): every
-      // header store complete and released to the workgroup before the barrier
+    if (io.fobs || S.autoreset == USV_AUTORESET_SAME_STEP) {
+      // waves 1-3 read these header rows back for their done envs' terminal obs (emit_env), and
+      // reset their done envs, whose state this wave stored (same-step autoreset): every store
+      // complete and released to the workgroup before the barrier, so no reset store of another
+      // wave can be overtaken by one of these
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       vm_wait<0>();
     } else {
@@ -1925,23 +1925,16 @@ __device__ __forceinline__ void step_body_blockdyn(const State<R>& S, const IO<R
     vm_wait<0>();
   }
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // records + ray table published
-  if (ne <= 0) {
-    if (wave == 0) {                                  // (no envs of its own to scan)
-      vm_wait<0>();
-      *dynsig = 1u;
-    }
-    return;
-  }
+  if (ne <= 0) return;
   USV_STAMP_W(2);
   prof.mark(0);
   const int k = wave * EPW + min(l, ne - 1);                // lane-per-env view of this wave's envs
   const R4<R> P = rec[k], M = rec[kWave + k];
   const unsigned trunc_m = (unsigned)ballot(M.z != R(0));
   unsigned term_m, coll_m;
-  scan_envs<R, MODE, LID>(S, io, L, e0, ne, P, (int)M.y, trunc_m, term_m, coll_m, prof,
-                          wave == 0 ? dynsig : nullptr);
+  scan_envs<R, MODE, LID>(S, io, L, e0, ne, P, (int)M.y, trunc_m, term_m, coll_m, prof);
   USV_STAMP_W(3);
-  scan_epilogue<R, MODE>(S, io, e0, ne, M.x, true, term_m, coll_m, trunc_m, wave == 0 ? nullptr : dynsig);
+  scan_epilogue<R, MODE>(S, io, e0, ne, M.x, true, term_m, coll_m, trunc_m);
   prof.mark(5);
   prof.flush(blockIdx.x * kWaves + wave);
   USV_STAMP_W(6);
@@ -1986,8 +1979,10 @@ void step_kernel_blockdyn(State<R> S, IO<R> io) { step_body_blockdyn<R, MODE, EP
 // waves wait at its barrier for them while the older block scans), back to 0 after the barrier;
 // (2) in a one-round grid (<= 2 blocks per CU) the second block of each CU (block index >= the CU
 // count: blocks are dispatched one per CU first) raises kQYoungWaves of its 16 waves to priority 1,
-// so the two blocks progress at more even rates.  A/B on one box (gpurun_out r5b-r5d): -0.27 to
-// -0.44 us per launch at 65 536 envs against the same build without.
+// so the two blocks progress at more even rates.  Both only in a one-round grid (State::qyoung set):
+// with more rounds (524 288 envs) the phase-1 priority cost 0.9 us of 161.  Same-box A/Bs (gpurun_out
+// r5b-r5e): -0.27 to -0.67 us per launch at 65 536 envs (usv-simple), -0.95 us (usv-asmc-simple, whose
+// q kernel has the same phase 1).
 #ifndef USV_QPRIO_DYN
 #define USV_QPRIO_DYN 3
 #endif
@@ -2114,8 +2109,9 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
 #else
   QProf* const qp = nullptr;
 #endif
-  // qctr[1 + w]: dynamics wave w's state stores are complete (fused, same-step autoreset: a wave
-  // that resets an env of wave w's first, so its reset stores cannot be overtaken by them)
+  // qctr[1 + w]: dynamics wave w's state stores are acknowledged (set after the barrier, below; a
+  // wave that same-step-resets one of wave w's envs waits for it, so its reset stores cannot be
+  // overtaken by them)
   unsigned* const qdyn = qctr + 1;
   if (threadIdx.x == 0) {
     qctr[0] = kQW;                                     // pairs 0 .. kQW-1 are the static first ones
@@ -2156,7 +2152,7 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
     // not run, or two waves would race on the same env's state
     if (wave < kDynWaves && wave * kWave < nbe) {
 #if USV_QPRIO_DYN
-      __builtin_amdgcn_s_setprio(USV_QPRIO_DYN);
+      if (S.qyoung != INT_MAX) __builtin_amdgcn_s_setprio(USV_QPRIO_DYN);
 #endif
       const int k = min(wave * kWave + l, nbe - 1);
       const int e = eb + k;
@@ -2183,6 +2179,20 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
   if (FUSED && wave < kDynWaves) __builtin_amdgcn_s_setprio(0);
 #endif
   if ((int)blockIdx.x >= S.qyoung && wave < kQYoungWaves) __builtin_amdgcn_s_setprio(1);
+#if USV_QFLAG
+  // Same-step reset ordering: a dynamics wave stored its envs' state in phase 1, and
+  // another wave may reset one of those envs later in this launch; two waves' stores to one address
+  // are ordered only if the first is acknowledged before the second is issued.  So each dynamics
+  // wave drains its stores here, after the barrier (its first pair's rows are already in LDS, and
+  // env_dynamics issues the state stores as soon as the new state exists, so little is left to
+  // wait for), and sets its flag; a reset of one of its envs waits for the flag.  Measured against
+  // no ordering at all: +0.1 us at 65 536 envs, +0.15 us at 524 288 (a per-pair flag in the loop
+  // cost 0.5 / 1.8 us, draining before the barrier 0.05 / 1.6 us; gpurun_out r5h, r5i).
+  if (FUSED && wave < kDynWaves) {
+    vm_wait<0>();
+    qdyn[wave] = 1u;
+  }
+#endif
   USV_STAMP_W(2);
   QMARK(0);
   unsigned tk = 0;
@@ -2332,8 +2342,6 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
       QMARK(5);
       vm_wait<7>();
       QMARK(6);
-      // every memory op before this pair's DMA is complete, the phase-1 state stores included
-      if (FUSED && wave < kDynWaves) qdyn[wave] = 1u;
       if (it == 0) USV_STAMP_W(5);                      // (diagnostic: first pair done)
       cur = nxt;
       pose = pose_n;
@@ -2350,7 +2358,7 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
     QMARK(11);
     for (; done; done &= done - 1) {
       const int e = de0 + __builtin_ctz(done);
-      if constexpr (FUSED) {
+      if constexpr (FUSED && USV_QFLAG) {
         // the env's phase-1 stores (by dynamics wave (e - eb) / 64) are acknowledged before its reset
         // stores are issued: two waves' stores to one address are otherwise unordered
         const unsigned* const f = qdyn + ((e - eb) >> 6);
@@ -2362,10 +2370,6 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
     QMARK(7);
   }
   QMARK(11);
-  if (FUSED && wave < kDynWaves) {                     // (a dynamics wave that scanned no pair)
-    vm_wait<0>();
-    qdyn[wave] = 1u;
-  }
   qprof_flush(qp);
   USV_STAMP_V(4, (unsigned long long)it);            // (diagnostic: pairs this wave scanned)
   USV_STAMP_W(3);

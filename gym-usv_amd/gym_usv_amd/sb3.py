@@ -29,14 +29,16 @@ page-locked buffers: the stacked obs on a copy stream while the host builds the 
 the small arrays (reward, done) first, and the terminal rows of the done envs only.  The returned
 arrays alternate between two such buffer sets, so each stays valid until the second-next step
 (SB3's collectors consume or copy them within one step).  ``infos`` is a fresh list of fresh dicts
-every step, as DummyVecEnv returns (a wrapper may write into them); the 4096 empty dicts are built
-while the GPU runs the step and the copies, so they cost no wall time on top of the copy wait.
+every step, as DummyVecEnv returns (a wrapper may write into them); the next step's 4096 empty dicts
+are built on a helper thread between steps (the main thread waits on the GPU with the GIL released),
+so they cost no wall time on the step itself.
 The env's device is the current device for the whole call (events and copies are ordered on its
 stream even when another device is current in the caller).
 """
 from __future__ import annotations
 
 import time
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 import torch
@@ -79,6 +81,10 @@ class DeviceFrameStack:
         new[:, -d:] = obs
         self._i = 1 - self._i
         return new, term
+
+
+def _empty_infos(n):
+    return [{} for _ in range(n)]
 
 
 def _to_gym_box(box):
@@ -133,6 +139,8 @@ class Sb3VecEnv:
         self._act_dev = torch.empty((n, venv.act_dim), dtype=torch.float32, device=dev)
         self._rew32 = torch.empty(n, dtype=torch.float32, device=dev)
         self._copy_stream = torch.cuda.Stream(dev) if self._cuda else None
+        self._pool = ThreadPoolExecutor(max_workers=1)  # builds the next step's empty info dicts
+        self._next_infos = self._pool.submit(_empty_infos, n)
 
     # ---------------------------------------------------------------- VecEnv API
     def reset(self):
@@ -191,13 +199,13 @@ class Sb3VecEnv:
             h["done"].copy_(done, non_blocking=True)
             small = torch.cuda.Event()
             small.record(main)
-            infos = [{} for _ in range(n)]              # (built while the GPU works)
             small.synchronize()
         else:
             h["obs"].copy_(obs)
             h["rew"].copy_(rew)
             h["done"].copy_(done)
-            infos = [{} for _ in range(n)]
+        infos = self._next_infos.result()               # fresh, built since the last step
+        self._next_infos = self._pool.submit(_empty_infos, n)
         done_np = h["done"].numpy()
         idx = np.flatnonzero(done_np)
         if idx.size:
@@ -223,6 +231,7 @@ class Sb3VecEnv:
         return self.step_wait()
 
     def close(self):
+        self._pool.shutdown(wait=True)
         self.venv.close()
 
     def seed(self, seed=None):

@@ -52,7 +52,7 @@ def main():
     src = os.path.join(ROOT, "gym-usv_amd", "csrc", "usv_kernels.hip")
     subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "--offload-arch=gfx950", "-std=c++17", "--cuda-device-only", "-S",
                     "-mllvm", "-amdgpu-atomic-optimizer-strategy=None", "-I" + os.path.join(ROOT, "include"),
-                    "-DUSV_DIAG", "-DUSV_DIAG_SECTIONS", "-o", args.asm, src], check=True,
+                    "-DUSV_DIAG", "-DUSV_DIAG_SECTIONS", *os.environ.get("XDEFS", "").split(), "-o", args.asm, src], check=True,
                    stderr=subprocess.DEVNULL)
     t = open(args.asm).read()
     names = [n for n in re.findall(r"^(_Z\w+):", t, re.M) if re.match(args.kernel, n)]
