@@ -28,17 +28,18 @@ The step itself stays on the GPU; only the arrays SB3 consumes are copied to the
 page-locked buffers: the stacked obs on a copy stream while the host builds the done envs' infos,
 the small arrays (reward, done) first, and the terminal rows of the done envs only.  The returned
 arrays alternate between two such buffer sets, so each stays valid until the second-next step
-(SB3's collectors consume or copy them within one step).  ``infos`` is a fresh list of fresh dicts
-every step, as DummyVecEnv returns (a wrapper may write into them); the next step's 4096 empty dicts
-are built on a helper thread between steps (the main thread waits on the GPU with the GIL released),
-so they cost no wall time on the step itself.
+(SB3's collectors consume or copy them within one step).  ``infos`` is a new list every step; a done
+env's info is a new dict; an env that did not end gets an empty dict that is reused across steps
+only while it stays empty: a dict a wrapper or callback wrote into is replaced by a new one before
+the next step (one C-level ``any()`` over the list detects it), so no write ever shows up in a
+later step's infos -- what DummyVecEnv's fresh dicts guarantee -- without building 4096 dicts per
+step (~0.1-0.2 ms of Python).
 The env's device is the current device for the whole call (events and copies are ordered on its
 stream even when another device is current in the caller).
 """
 from __future__ import annotations
 
 import time
-from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 import torch
@@ -81,10 +82,6 @@ class DeviceFrameStack:
         new[:, -d:] = obs
         self._i = 1 - self._i
         return new, term
-
-
-def _empty_infos(n):
-    return [{} for _ in range(n)]
 
 
 def _to_gym_box(box):
@@ -139,8 +136,8 @@ class Sb3VecEnv:
         self._act_dev = torch.empty((n, venv.act_dim), dtype=torch.float32, device=dev)
         self._rew32 = torch.empty(n, dtype=torch.float32, device=dev)
         self._copy_stream = torch.cuda.Stream(dev) if self._cuda else None
-        self._pool = ThreadPoolExecutor(max_workers=1)  # builds the next step's empty info dicts
-        self._next_infos = self._pool.submit(_empty_infos, n)
+        self._infos = [{} for _ in range(n)]            # per env: empty unless it ended this step
+        self._filled = np.empty(0, dtype=np.int64)
 
     # ---------------------------------------------------------------- VecEnv API
     def reset(self):
@@ -204,8 +201,13 @@ class Sb3VecEnv:
             h["obs"].copy_(obs)
             h["rew"].copy_(rew)
             h["done"].copy_(done)
-        infos = self._next_infos.result()               # fresh, built since the last step
-        self._next_infos = self._pool.submit(_empty_infos, n)
+        infos = self._infos
+        for i in self._filled:                          # last step's done envs: new empty dicts
+            infos[i] = {}
+        if any(infos):                                  # a consumer wrote into an empty info dict:
+            for i, d in enumerate(infos):               # replace it (theirs keeps the write)
+                if d:
+                    infos[i] = {}
         done_np = h["done"].numpy()
         idx = np.flatnonzero(done_np)
         if idx.size:
@@ -222,16 +224,16 @@ class Sb3VecEnv:
             for j, i in enumerate(idx):
                 infos[i] = {"terminal_observation": term_obs[j], "TimeLimit.truncated": bool(pack[j, w]),
                                   "episode": {"r": round(float(pack[j, w + 1]), 6), "l": int(pack[j, w + 2]), "t": t}}
+        self._filled = idx
         if self._cuda:
             obs_done.synchronize()
-        return h["obs"].numpy(), h["rew"].numpy(), done_np, infos
+        return h["obs"].numpy(), h["rew"].numpy(), done_np, list(infos)
 
     def step(self, actions):
         self.step_async(actions)
         return self.step_wait()
 
     def close(self):
-        self._pool.shutdown(wait=True)
         self.venv.close()
 
     def seed(self, seed=None):
