@@ -74,11 +74,14 @@ class UsvAsmcBatch:
         a = self._dev(action, 2)
         p = self._dev(position, 3)
         v = self._dev(velocity, 3)
-        rc = self.lib.usv_asmc_compute(self.precision, self.n, ctypes.c_void_p(a.data_ptr()),
-                                       ctypes.c_void_p(p.data_ptr()), ctypes.c_void_p(v.data_ptr()),
-                                       ctypes.c_void_p(self.state.data_ptr()),
-                                       ctypes.c_void_p(self.perturb_step.data_ptr()), int(bool(do_perturb)),
-                                       int(calls), _stream(self.device))
+        # the library launches on the current device: make it this batch's, with the
+        # launch on that device's current stream
+        with torch.cuda.device(self.device):
+            rc = self.lib.usv_asmc_compute(self.precision, self.n, ctypes.c_void_p(a.data_ptr()),
+                                           ctypes.c_void_p(p.data_ptr()), ctypes.c_void_p(v.data_ptr()),
+                                           ctypes.c_void_p(self.state.data_ptr()),
+                                           ctypes.c_void_p(self.perturb_step.data_ptr()), int(bool(do_perturb)),
+                                           int(calls), _stream(self.device))
         _lib.check(rc, self.lib)
         return p, v
 

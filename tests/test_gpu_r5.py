@@ -73,3 +73,33 @@ def test_heading_set_rejects_unrepresentable_turns(bad):
     got = env.get_field("psi")
     assert abs(got[5] - 1e9) <= 2 * np.pi * 2 ** -23 * 4   # phi in [-pi, pi] rounded to f32
     env.close()
+
+
+@pytest.mark.parametrize("env_id,n", [("usv-simple", 40000), ("usv-simple", 65536), ("usv-simple", 60001),
+                                      ("usv-asmc-simple", 65536), ("usv-asmc-simple", 33001)])
+def test_xcd_weighted_blocks_bit_identical(env_id, n):
+    """One-round grids of the 128-env block queue give the blocks on late-starting XCDs fewer envs
+    (State::qsplit: 8 consecutive blocks own 1 024 envs in per-XCD shares).  Bit-identical to the
+    split kind 4 (same queue, dynamics in their own launch) and to the fused wave kernel (kind 1),
+    over a rollout with same-step resets, at counts that leave the last 8-block group partial."""
+    T, limit = 24, 9
+    fused = "128,7,6" if env_id == "usv-asmc-simple" else "128,7,5"
+    ref = None
+    for v in (fused, "128,7,4", "16,7,1"):
+        gen = torch.Generator(device="cuda").manual_seed(4)
+        env = make(env_id, n, seed=31, max_episode_steps=limit, kernel_variant=v, copy=False)
+        env.reset(seed=31)
+        outs = []
+        for _ in range(T):
+            a = torch.rand(n, 2, device="cuda", generator=gen) * torch.tensor([0.8, 2.0], device="cuda") \
+                + torch.tensor([0.2, -1.0], device="cuda")
+            o, r, te, tr, info = env.step(a)
+            outs.append(torch.cat([o.flatten(), r, te.float(), tr.float()]).cpu())
+        blob = env.state_blob()
+        env.close()
+        if ref is None:
+            ref = (outs, blob)
+            continue
+        for t, (x, y) in enumerate(zip(ref[0], outs)):
+            assert torch.equal(x, y), f"variant {v} differs from {fused} at step {t} (n={n})"
+        assert np.array_equal(ref[1], blob), f"variant {v}: state differs (n={n})"

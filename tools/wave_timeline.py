@@ -108,6 +108,14 @@ def main():
             m = blk_id == b
             per_cu.setdefault(int(cu_id[m][0]), []).append((float(st[m, 0].min()), float(st[m, 4].max()), int(b)))
         pairs = [sorted(x) for x in per_cu.values() if len(x) == 2]
+        # dispatch: is block b on XCD b % 8, and when does it start (by b % 8, by b // 8)
+        nb = nw // wpb
+        bx = np.array([int(xcc[b * wpb]) for b in range(nb)])
+        bs = np.array([float(st[b * wpb:(b + 1) * wpb, 0].min()) for b in range(nb)])
+        out["xcc_eq_block_mod8"] = round(float(np.mean(bx == np.arange(nb) % 8)), 3)
+        out["block_start_by_mod8"] = {int(x): round(float(bs[np.arange(nb) % 8 == x].mean()), 2) for x in range(8)}
+        grp = np.arange(nb) // 8
+        out["block_start_by_group_deciles"] = pct([bs[grp == q].mean() for q in np.unique(grp)])
         out["cus"] = len(per_cu)
         out["blocks_per_cu"] = pct([len(x) for x in per_cu.values()])
         if pairs:
