@@ -69,7 +69,6 @@ template <typename R> struct State {
   int rowspan;             // block-queue step: store an env pair's obs rows as one 32-B-aligned span
   int qyoung;              // block-queue step: blocks from this index raise kQYoungWaves waves' issue
                            //   priority (a CU's second block of a one-round grid; INT_MAX: none)
-  uint64_t qsplit;         // block-queue step: env pairs per block by XCD (8 x 8 bits; 0: 128 envs each)
   int fstride;             // elements between fields (>= N, 256-B aligned)
   int ostride;             // obstacle plane stride: cap rounded up to a multiple of 4
   uint64_t seed, gid0;
@@ -1991,17 +1990,7 @@ void step_kernel_blockdyn(State<R> S, IO<R> io) { step_body_blockdyn<R, MODE, EP
 #define USV_QPRIO_YOUNG 10
 #endif
 constexpr int kQYoungWaves = USV_QPRIO_YOUNG;
-#ifndef USV_QE_CAP
-#define USV_QE_CAP 136   // env capacity of a 128-env block (State::qsplit gives XCD-weighted blocks up to this)
-#endif
-#ifndef USV_QPRIO_LAST
-#define USV_QPRIO_LAST 0   // experiment: issue priority of a wave's last pair (the queue is dry)
-#endif
-#ifndef USV_QSPLIT_TABLE
-#define USV_QSPLIT_TABLE 0   // per-XCD block weights (qsplit_table): 0 = uniform until measured
-#endif
-constexpr int kQW = USV_QW, kQE = USV_QE, kQRec = 16, kQECap = USV_QE_CAP;
-static_assert(kQECap >= kQE && kQECap % 2 == 0, "block capacity");
+constexpr int kQW = USV_QW, kQE = USV_QE, kQRec = 16;
 __host__ __device__ constexpr size_t q_slice_bytes() { return 256 * 8 + 64 * 4 + 2 * 1024; }
 
 // One DMA instruction (<= 64 pieces of 16 B, i.e. <= 1 KiB): pieces c >= nchunk are not copied.
@@ -2085,7 +2074,7 @@ constexpr int kQSmallBelow = 32768;   // env count below which the small blocks 
 template <int QE = kQE, int QW = kQW> __host__ __device__ constexpr size_t lds_q_bytes() {
   return wave_tab_bytes<float>() + QW * q_slice_bytes() + QE * kQRec * 4 + 16 + QE * 4;   // + n_obs[QE]
 }
-static_assert(2 * lds_q_bytes<kQECap, kQW>() <= 160 * 1024, "two blocks per CU");
+static_assert(2 * lds_q_bytes() <= 160 * 1024, "two blocks per CU");
 static_assert(4 * lds_q_bytes<kQE_S, kQW_S>() <= 160 * 1024, "four small blocks per CU");
 
 // DONE: also write the done mask (io.done, ABI v4).  A template switch rather than a runtime test:
@@ -2102,21 +2091,8 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const int l = lane_id();
   constexpr int os = 32, rowb = row_bytes<float>(32);  // cap in [29, 32]: plane stride 32, 384-B rows
-  // this block's envs: eb .. eb + nbe - 1.  kQE is the block's capacity; the 128-env blocks own 128
-  // envs each, or (State::qsplit, a one-round grid) the per-XCD pair counts packed in qsplit: block b
-  // runs on XCD b % 8 (dispatch is round-robin over the XCDs) and 8 consecutive blocks own 1 024 envs
-  int eb, nbe;
-  if (kQE != kQE_S && S.qsplit != 0ull) {
-    const int x = blockIdx.x & 7;
-    int pre = 0;
-    for (int i = 0; i < x; ++i) pre += (int)((S.qsplit >> (8 * i)) & 0xffull);
-    eb = (int)(blockIdx.x >> 3) * (8 * ::usv::kQE) + 2 * pre;
-    nbe = min(2 * (int)((S.qsplit >> (8 * x)) & 0xffull), S.N - eb);
-  } else {
-    constexpr int nom = kQE == kQE_S ? kQE_S : ::usv::kQE;
-    eb = blockIdx.x * nom;
-    nbe = min(nom, S.N - eb);
-  }
+  const int eb = blockIdx.x * kQE;                     // this block's envs: eb .. eb + nbe - 1
+  const int nbe = min(kQE, S.N - eb);
   const int np = (nbe + 1) >> 1;                       // and pairs 0 .. np - 1 (block-local)
   char* const slice = lds + wave_tab_bytes<float>() + wave * q_slice_bytes();
   unsigned long long* const slot = reinterpret_cast<unsigned long long*>(slice);
@@ -2141,7 +2117,6 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
     qctr[0] = kQW;                                     // pairs 0 .. kQW-1 are the static first ones
     qdyn[0] = 0u;
     qdyn[1] = 0u;
-    qdyn[2] = 0u;
   }
 
   // the ray table: by the last wave, so that the dynamics waves (fused) issue no DMA of their own
@@ -2191,7 +2166,7 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
       make_qrec(recs + k * kQRec, px, py, sp, cp, partial, 0, trunc, hdr);   // (n_obs: qnob)
     }
   } else {
-    if (wave < (kQE + 15) / 16 && wave * 16 < nbe)     // 16 records (1 KiB) per wave
+    if (wave < kQE / 16 && wave * 16 < nbe)            // 16 records (1 KiB) per wave
       dma_copy1(S.qrec + (size_t)(eb + wave * 16) * kQRec, recs + wave * 16 * kQRec, min(16, nbe - wave * 16) * kQRec * 4);
   }
   // rows, ray table and records landed (the dynamics waves issued no DMA: their stores drain later,
@@ -2295,11 +2270,6 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
         dma_copy_at(oblk, 2 * rowb * nxt, nbuf, (pair_hasb(nxt) ? 2 : 1) * rowb);
 #endif
       }
-#if USV_QPRIO_LAST
-      else {
-        __builtin_amdgcn_s_setprio(USV_QPRIO_LAST);    // the queue is dry: this wave's last pair first
-      }
-#endif
       // this lane's env: lanes 0..31 env A, 32..63 env B (env A again when there is no B)
       const int kl = (hb && hasB) ? k0 + 1 : k0;
       const int el = e0 + (kl - k0);
@@ -2408,7 +2378,7 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
 
 template <int MODE, bool FUSED, bool DONE, bool CHAIN = true, bool INFO = false, bool SPAN = false>
 __global__ __launch_bounds__(kQW * kWave) __attribute__((amdgpu_num_sgpr(USV_QSGPR), amdgpu_waves_per_eu(USV_QWPE, USV_QWPE)))
-void step_q_kernel(State<float> S, IO<float> io) { step_q_body<MODE, FUSED, DONE, kQECap, kQW, CHAIN, INFO, SPAN>(S, io); }
+void step_q_kernel(State<float> S, IO<float> io) { step_q_body<MODE, FUSED, DONE, kQE, kQW, CHAIN, INFO, SPAN>(S, io); }
 template <int MODE, bool DONE, bool CHAIN = true, bool INFO = false>
 __global__ __launch_bounds__(kQW_S * kWave) __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8)))
 void step_qs_kernel(State<float> S, IO<float> io) { step_q_body<MODE, true, DONE, kQE_S, kQW_S, CHAIN, INFO>(S, io); }
@@ -2982,7 +2952,6 @@ int carve(Handle* h, State<R>& S) {
   S.prio = h->prio;
   S.rowspan = h->cfg.num_envs >= kRowSpanFrom;
   S.qyoung = INT_MAX;                                    // (set per launch: launch_step)
-  S.qsplit = 0ull;
   S.seed = h->cfg.seed;
   S.gid0 = h->cfg.env_id_offset;
   // ray offsets start + i*res (usv_asmc_ca_env.py:420), cos/sin in float64 on the host
@@ -3078,7 +3047,6 @@ void* pick_q(int mode, bool fused, bool small = false, bool done = false, bool s
 template <typename R>
 int launch_step_kernels(Handle* h, State<R>& S, const float* act, float* obs, void* rew, uint8_t* term,
                         uint8_t* trunc, uint8_t* done, float* fobs, void* info, hipStream_t st);
-uint64_t qsplit_table();
 
 // The step, then (NumPy-exact reset mode) the resets of the envs that ended in it.
 template <typename R>
@@ -3130,17 +3098,13 @@ int launch_step_kernels(Handle* h, State<R>& S, const float* act, float* obs, vo
         HIP_TRY(hipLaunchKernel((void*)&asmc_chain_kernel<float>, dim3((S.N + kBlock - 1) / kBlock), dim3(kBlock), args, 0, st));
       const bool small = h->kind != 4 && h->epb == kQE_S;
       const int qe = small ? kQE_S : kQE, qw = small ? kQW_S : kQW;
-      // a one-round grid of the 128-env blocks: the second block of each CU raises priority, and
-      // the blocks on the XCDs that start late own fewer envs (State::qsplit)
-      int nblk = (S.N + qe - 1) / qe;
-      const bool one_round = !small && nblk > h->cus && nblk <= 2 * h->cus;
-      S.qsplit = one_round ? qsplit_table() : 0ull;
-      if (S.qsplit) nblk = (S.N + 8 * kQE - 1) / (8 * kQE) * 8;
-      S.qyoung = one_round ? h->cus : INT_MAX;
+      // a one-round grid of the 128-env blocks: the second block of each CU raises priority
+      const int nblk = (S.N + qe - 1) / qe;
+      S.qyoung = (!small && nblk > h->cus && nblk <= 2 * h->cus) ? h->cus : INT_MAX;
       HIP_TRY(hipLaunchKernel(pick_q(h->cfg.mode, h->kind != 4, small, io.done != nullptr, h->kind == 6,
                                      io.info != nullptr, S.rowspan != 0),
-                              dim3(nblk), dim3(qw * kWave), args,
-                              small ? lds_q_bytes<kQE_S, kQW_S>() : lds_q_bytes<kQECap, kQW>(), st));
+                              dim3((S.N + qe - 1) / qe), dim3(qw * kWave), args,
+                              small ? lds_q_bytes<kQE_S, kQW_S>() : lds_q_bytes(), st));
       return USV_OK;
     }
   }
@@ -3404,32 +3368,6 @@ int set_experiment(Handle* h, State<R>& S, const usv_experiment* x) {
   return USV_OK;
 }
 
-// Env pairs per 128-env block by XCD for a one-round grid (State::qsplit; 8 consecutive blocks own
-// 512 pairs).  Block b runs on XCD b % 8, and the XCDs do not start together: in every per-wave
-// timeline (r02, r04, r05: tools/wave_timeline.py) XCD 0 starts first and XCDs 4, 5 and 7 up to
-// ~1.2 us later, while a CU's busy time is the same on every XCD -- so the late XCDs' CUs set the
-// launch's end.  Their blocks get fewer pairs, the early XCDs' more.
-uint64_t qsplit_table() {
-#if USV_QSPLIT_TABLE == 1
-  constexpr int p[8] = {66, 65, 65, 64, 62, 62, 65, 63};
-#elif USV_QSPLIT_TABLE == 2
-  constexpr int p[8] = {68, 66, 66, 64, 60, 60, 66, 62};
-#else
-  constexpr int p[8] = {64, 64, 64, 64, 64, 64, 64, 64};
-#endif
-  static_assert(p[0] + p[1] + p[2] + p[3] + p[4] + p[5] + p[6] + p[7] == 4 * kQE, "8 blocks own 8 x 128 envs");
-  uint64_t v = 0;
-  for (int i = 0; i < 8; ++i) {
-    if (2 * p[i] > kQECap) return 0;                   // (beyond the block's capacity: uniform)
-    v |= (uint64_t)p[i] << (8 * i);
-  }
-#if USV_QSPLIT_TABLE == 0
-  return 0;
-#else
-  return v;
-#endif
-}
-
 // The block-queue step's LDS exceeds the 64 KiB default: raise the kernels' dynamic-LDS limit.
 int queue_lds_attr(const Handle* h) {
   if (h->kind != 4 && h->kind != 5 && h->kind != 6) return USV_OK;
@@ -3438,7 +3376,7 @@ int queue_lds_attr(const Handle* h) {
     for (const bool info : {false, true}) {
       for (const bool span : {false, true})
         HIP_TRY(hipFuncSetAttribute(pick_q(h->cfg.mode, h->kind != 4, false, done, split, info, span),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_q_bytes<kQECap, kQW>()));
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_q_bytes()));
       if (h->kind != 4)
         HIP_TRY(hipFuncSetAttribute(pick_q(h->cfg.mode, true, true, done, split, info),
                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_q_bytes<kQE_S, kQW_S>()));

@@ -77,11 +77,11 @@ def test_heading_set_rejects_unrepresentable_turns(bad):
 
 @pytest.mark.parametrize("env_id,n", [("usv-simple", 40000), ("usv-simple", 65536), ("usv-simple", 60001),
                                       ("usv-asmc-simple", 65536), ("usv-asmc-simple", 33001)])
-def test_xcd_weighted_blocks_bit_identical(env_id, n):
-    """One-round grids of the 128-env block queue give the blocks on late-starting XCDs fewer envs
-    (State::qsplit: 8 consecutive blocks own 1 024 envs in per-XCD shares).  Bit-identical to the
-    split kind 4 (same queue, dynamics in their own launch) and to the fused wave kernel (kind 1),
-    over a rollout with same-step resets, at counts that leave the last 8-block group partial."""
+def test_one_round_grid_bit_identical(env_id, n):
+    """One-round grids of the 128-env block queue (<= 2 blocks per CU) run the round-5 priority path
+    (phase-1 priority, the second blocks' raised waves, the dynamics waves' drain and flag):
+    bit-identical to the split kind 4 (same queue, dynamics in their own launch) and to the fused
+    wave kernel (kind 1), over a rollout with same-step resets, at full and ragged counts."""
     T, limit = 24, 9
     fused = "128,7,6" if env_id == "usv-asmc-simple" else "128,7,5"
     ref = None

@@ -99,3 +99,23 @@ def test_timed_window_is_collective_free():
         assert inside == [], f"rank {rank}: collectives inside the timed window: {inside}"
         assert names.count("barrier") == 2 and "all_reduce" in names   # before t0, after t1, the max
         assert el == pytest.approx(max(r[4] for r in res))
+
+
+def test_committed_counters_cover_the_driver_line():
+    """The driver's bench line reads roofline.traffic / valu_frac for the headline workload and the
+    f64 leg from profiles/pmc_summary.json: both keys exist there with per-launch bytes above the
+    algorithmic bytes (counter-backed traffic, not a model)."""
+    import json
+    import os
+    import bench
+    pmc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "pmc_summary.json")
+    for prec in ("f32", "f64"):
+        traffic, valu = bench.pmc_entry(pmc, f"usv-simple/65536/{prec}/window")
+        assert traffic and valu, prec
+        algo = bench.algorithmic_bytes_per_env_step("usv-simple", 21.9, prec) * 65536
+        assert 1.0 <= traffic / algo < 1.6, (prec, traffic / algo)
+    for key in ("usv-asmc-simple/65536/f32/window", "usv-asmc-simple/65536/f64/window",
+                "usv-simple/524288/f32/window"):
+        assert all(bench.pmc_entry(pmc, key)), key
+    assert bench.pmc_entry(pmc, "no/such/key") == (None, None)
+    assert json.load(open(pmc))["usv-simple/65536/f32/window"]["round"].startswith("r05")
