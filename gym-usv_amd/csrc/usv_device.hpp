@@ -395,6 +395,30 @@ __device__ __forceinline__ void asmc_substep(R (&s)[kAsmcN], R a0, R a1, R& x, R
 //    read inside the substep, so xl, yl accumulate their increments and the caller adds them after the
 //    20 substeps; psi is read by the next substep, so it integrates with compensated summation (pl
 //    carries what each addition rounded away; golden replay reward error 1.0e-4 -> 3.5e-5).
+// End of a run of f32 substeps: the pose from what asmc_substep_f32 accumulated.  Round 5: xl, yl, pl
+// are the sums of the rates x', y', r over the run, and each trapezoid sum is telescoped,
+// sum_k h2 (q_k + q_{k-1}) = h2 (2 sum - q_last + q_{-1}) (q_{-1} = s[4], s[5], s[6] before the run:
+// e0 = {x4, y5, r6}); psi0 is the heading before the run (inside the run psi integrates as usual,
+// since the substeps read it).  v1: xl, yl the increments, pl the compensated summation's error.
+struct AsmcRun { float x4, y5, r6, psi0; };
+__device__ __forceinline__ AsmcRun asmc_run_begin(const float (&s)[kAsmcN], float psi) {
+  return AsmcRun{s[4], s[5], s[6], psi};
+}
+__device__ __forceinline__ void asmc_run_end(float& x, float& y, float& psi, float xl, float yl, float pl,
+                                             const AsmcRun& e0, const float (&s)[kAsmcN]) {
+#ifndef USV_ASMC_F32_V1
+  constexpr float h2 = float(H / 2);
+  x += h2 * (fmaf(2.0f, xl, -s[4]) + e0.x4);
+  y += h2 * (fmaf(2.0f, yl, -s[5]) + e0.y5);
+  psi = e0.psi0 + h2 * (fmaf(2.0f, pl, -s[6]) + e0.r6);
+#else
+  (void)e0; (void)s;
+  x += xl;
+  y += yl;
+  psi += pl;
+#endif
+}
+
 #ifndef USV_ASMC_F32_V1
 // asin on [-1, 1] for the f32 substep: |x| < 1/2 as s + s t P(t) with t = x^2, else
 // pi/2 - 2 asin(sqrt((1 - |x|) / 2)) with the same polynomial (Cephes asinf's minimax P, ~2.5e-7
@@ -410,98 +434,6 @@ __device__ __forceinline__ float asin_f32(float x) {
   return copysignf(big ? fmaf(-2.0f, as, 1.57079632679f) : as, x);
 }
 
-#ifdef USV_ASMC_F32_V3
-// Round 5, v3: the same substep as v2 below, reassociated for a short loop-carried chain.  A lone wave
-// per SIMD issues one VALU per ~4 cycles but waits ~8 on each dependent one, so the chain
-// r, psi -> psi_d -> r_d -> filter -> sigma_psi -> gain / root -> tau_z -> r' -> r sets the substep's
-// time.  Identities in real arithmetic only:
-//  * the third-order filter (:86-88) is linear in r_d: o'' = 4 r_d - 4 (s1 + s2),
-//    o' = s2 + h2 s3 + 4 h2 (r_d - s1 - s2), o = s1 + h2 (2 s2 + h2 s3) + 4 h2^2 (r_d - s1 - s2):
-//    one fma each after r_d, the rest from the state;
-//  * the velocity updates u += h2 (u' + u'_last) etc. with u' = ... + c ua: the terms that do not wait
-//    for the control law are summed first, so each velocity is one fma after its root.
-__device__ __forceinline__ void asmc_substep_f32(float (&s)[kAsmcN], float a0, float a1, float& x, float& y,
-                                                 float& psi, float& u, float& v, float& r, float& xl, float& yl,
-                                                 float& pl, float kt, int pstep = 0, bool perturb = false) {
-  constexpr float h2 = float(H / 2);
-  const float au = fabsf(u), av = fabsf(v), ar = fabsf(r);
-  const float vmag = __builtin_amdgcn_sqrtf(fmaf(u, u, v * v));
-  // J(psi_old) (:179), off the chain
-  const float pr = fmaf(kt, 1.74845553e-07f, fmaf(-kt, 6.28318548f, psi));
-  const float sp = __sinf(pr), cp = __cosf(pr);
-  // yaw channel (:72-89, :119-121, :134)
-  const float beta = asin_f32(v * __builtin_amdgcn_rcpf(0.001f + vmag));
-  const float psi_d = psi + beta + a1;
-  const float r_d = (psi_d - s[0]) * float(1.0 / H);
-  s[0] = psi_d;
-  const float s12 = s[1] + s[2];
-  const float o_dd = fmaf(4.0f, r_d, -4.0f * s12);
-  const float o_d = fmaf(4.0f * h2, r_d, fmaf(-4.0f * h2, s12, fmaf(h2, s[3], s[2])));
-  const float o = fmaf(4.0f * h2 * h2, r_d, fmaf(-4.0f * h2 * h2, s12, fmaf(h2, fmaf(h2, s[3], 2.0f * s[2]), s[1])));
-  s[1] = o; s[2] = o_d; s[3] = o_dd;
-  const float e_psi = asmc_wrap(psi_d - psi);
-  const float sig_p = o + (float(LAMBDA_PSI) * e_psi - r);
-  // surge channel (:128-133)
-  const float e_u = a0 - u;
-  s[13] = fmaf(e_u + s[10], h2, s[13]);
-  s[10] = e_u;
-  const float sig_u = fmaf(float(LAMBDA_U), s[13], e_u);
-  // adaptive gains (:137-146); the roots' sign-carrying square roots (:150-151) in parallel
-  const float kdu = s[14] > float(KMIN_U) ? copysignf(float(K_U), fabsf(sig_u) - float(MU_U)) : float(KMIN_U);
-  const float kdp = s[15] > float(KMIN_PSI) ? copysignf(float(K_PSI), fabsf(sig_p) - float(MU_PSI)) : float(KMIN_PSI);
-  s[14] = fmaf(kdu + s[11], h2, s[14]);
-  s[15] = fmaf(kdp + s[12], h2, s[15]);
-  s[11] = kdu; s[12] = kdp;
-  const float cs_u = copysignf(__builtin_amdgcn_sqrtf(fabsf(sig_u)), sig_u);
-  const float cs_p = copysignf(__builtin_amdgcn_sqrtf(fabsf(sig_p)), sig_p);
-  // lambda e - ua = T + Ka * cs (:150-151, :154-155)
-  const float t_u = fmaf(float(K2_U), sig_u, float(LAMBDA_U) * e_u);
-  const float t_p = fmaf(float(K2_PSI), sig_p, float(LAMBDA_PSI) * e_psi);
-  float p0 = 0.0f, p1 = 0.0f;
-  if (perturb) {                                                                // T += F @ J (:184-198)
-    double fx, fy;
-    perturb_force(pstep, fx, fy);
-    const float pfx = float(fx), pfy = float(fy);
-    p0 = pfx * cp + pfy * sp;
-    p1 = pfx * -sp + pfy * cp;
-  }
-  const float xuu = au > 1.2f ? -70.92f : 0.0f;                                 // :95-99 (Xu cancels)
-  const float qs = fmaf(xuu * au, 1.0f - u, fmaf(float(Y_R_DOT + N_V_DOT), r, float(Y_V_DOT) * v) * r);
-  const float md11 = fmaf(float(YV_K + YVV), av, float(YVR) * ar);
-  const float md12 = fmaf(float(YR_K), vmag, fmaf(float(YRV), av, float(YRR) * ar));
-  const float md21 = fmaf(float(NV_K), vmag, fmaf(float(NVV), av, float(NVR) * ar));
-  const float n22 = fmaf(float(NRV), av, float(NRR) * ar);
-  const float rhs1 = fmaf(md11, v, fmaf(fmaf(float(-(MASS - X_U_DOT * MASS)), u, md12), r, p1));
-  // rhs2 = (Iz - Nr') (t_p + Ka_psi cs_p) + w2
-  const float w2 = fmaf(u, fmaf(float(X_U_DOT + Y_V_DOT - X_U_DOT * MASS), v, float(Y_R_DOT + N_V_DOT) * r),
-                        fmaf(md21, v, n22 * r));
-  const float ap = fmaf(s[15], cs_p, t_p);                                      // lambda e_psi - ua_psi
-  const float au_ = fmaf(s[14], cs_u, t_u);                                     // lambda e_u - ua_u
-  const float rhs2 = fmaf(float(IZ - N_R_DOT), ap, w2);
-  const float ud = fmaf(float(MI00), p0 - qs, au_);                             // :226
-  const float vd = fmaf(float(MI11), rhs1, float(MI12) * rhs2);
-  const float rd = fmaf(float(MI21), rhs1, float(MI22) * rhs2);
-  // velocities (:228-229): v_new = (v + h2 (v'_last + v'_w)) + h2 c ap, v'_w the part without ap
-  constexpr float cv = float(H / 2 * MI12 * (IZ - N_R_DOT)), cr = float(H / 2 * MI22 * (IZ - N_R_DOT));
-  const float qv = fmaf(h2, s[8] + fmaf(float(MI11), rhs1, float(MI12) * w2), v);
-  const float qr = fmaf(h2, s[9] + fmaf(float(MI21), rhs1, float(MI22) * w2), r);
-  const float qu = fmaf(h2, s[7] + fmaf(float(MI00), p0 - qs, t_u), u);
-  u = fmaf(h2 * s[14], cs_u, qu);
-  v = fmaf(cv * s[15], cs_p, fmaf(cv, t_p, qv));
-  r = fmaf(cr * s[15], cs_p, fmaf(cr, t_p, qr));
-  s[7] = ud; s[8] = vd; s[9] = rd;
-  const float xd = fmaf(cp, u, -(sp * v)), yd = fmaf(sp, u, cp * v);          // :233
-  {                                                                             // :234
-    const float ix = (xd + s[4]) * h2, iy = (yd + s[5]) * h2, ip = fmaf(h2, r, h2 * s[6]);
-    xl += ix;
-    yl += iy;
-    const float sq = psi + ip;
-    pl += ip - (sq - psi);
-    psi = sq;
-  }
-  s[4] = xd; s[5] = yd; s[6] = r;
-}
-#else
 // Round 5: the rhs of M nu' = tau - C(nu) nu - D(nu) nu folded further (identities in real arithmetic,
 // with (Tx, 0, Tz) as in round 4):
 //  * surge: M00 = m - Xu', so u' = (lambda_u e_u - ua_u) - (Yv' v r + (Yr' + Nv') r^2 + Xuu |u| (1 - u)) / M00
@@ -522,23 +454,12 @@ __device__ __forceinline__ void asmc_substep_f32(float (&s)[kAsmcN], float a0, f
   const float psi_d = psi + beta + a1;
   const float r_d = (psi_d - s[0]) * float(1.0 / H);
   s[0] = psi_d;
-#ifdef USV_ASMC_FILTER_LIN
-  // the filter is linear in r_d (see v3): one fma each after r_d
-  const float s12 = s[1] + s[2];
-  const float o_dd = fmaf(4.0f, r_d, -4.0f * s12);
-  const float o_d = fmaf(4.0f * h2, r_d, fmaf(-4.0f * h2, s12, fmaf(h2, s[3], s[2])));
-  const float o = fmaf(4.0f * h2 * h2, r_d, fmaf(-4.0f * h2 * h2, s12, fmaf(h2, fmaf(h2, s[3], 2.0f * s[2]), s[1])));
-  s[1] = o; s[2] = o_d; s[3] = o_dd;
-  const float e_psi = asmc_wrap(psi_d - psi);
-  const float sig_p = o + (float(LAMBDA_PSI) * e_psi - r);
-#else
   const float o_dd = 4.0f * ((r_d - s[1]) - s[2]);
   const float o_d = fmaf(o_dd + s[3], h2, s[2]);
   const float o = fmaf(o_d + s[2], h2, s[1]);
   s[1] = o; s[2] = o_d; s[3] = o_dd;
   const float e_psi = asmc_wrap(psi_d - psi);
   const float sig_p = (o - r) + float(LAMBDA_PSI) * e_psi;
-#endif
   // surge channel (:128-133)
   const float e_u = a0 - u;
   s[13] = fmaf(e_u + s[10], h2, s[13]);
@@ -584,16 +505,14 @@ __device__ __forceinline__ void asmc_substep_f32(float (&s)[kAsmcN], float a0, f
   s[7] = ud; s[8] = vd; s[9] = rd;
   const float xd = fmaf(cp, u, -(sp * v)), yd = fmaf(sp, u, cp * v);          // :233
   {                                                                             // :234
-    const float ix = (xd + s[4]) * h2, iy = (yd + s[5]) * h2, ip = (r + s[6]) * h2;
-    xl += ix;
-    yl += iy;
-    const float sq = psi + ip;
-    pl += ip - (sq - psi);
-    psi = sq;
+    // xl, yl, pl sum the rates; the caller applies the telescoped trapezoid sums once (asmc_run_end)
+    xl += xd;
+    yl += yd;
+    pl += r;
+    psi = fmaf(r + s[6], h2, psi);
   }
   s[4] = xd; s[5] = yd; s[6] = r;
 }
-#endif  // USV_ASMC_F32_V3
 #else
 __device__ __forceinline__ void asmc_substep_f32(float (&s)[kAsmcN], float a0, float a1, float& x, float& y,
                                                  float& psi, float& u, float& v, float& r, float& xl, float& yl,

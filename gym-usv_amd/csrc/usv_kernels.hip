@@ -191,6 +191,11 @@ constexpr int kRowSpanFrom = 196608;
 #ifndef USV_QFLAG
 #define USV_QFLAG 3   // block queue: same-step resets wait for the dynamics waves' store flag (0: diagnostic off)
 #endif
+#ifndef USV_STATIC_PRIO
+// issue-priority mode of the static-split kinds 1-3 (State::prio: 1 ramp, 2 last iteration first, 0 none);
+// kind 3 f64 at 65 536 envs, same box: 1 -> 40.5 us, 0 -> 43.2, 2 -> 43.2
+#define USV_STATIC_PRIO 1
+#endif
 #ifndef USV_F64_REC_SOA
 #define USV_F64_REC_SOA 1   // lidar_wave2_d's per-obstacle records as two 16-B planes (round 5; 0: one 32-B record)
 #endif
@@ -618,8 +623,9 @@ __global__ __launch_bounds__(kBlock) void asmc_compute_kernel(int n, const R* __
     if constexpr (std::is_same<R, float>::value) {
       float xl = 0.0f, yl = 0.0f, pl = 0.0f;
       const float kt = rintf(psi * 0.159154943f);
+      const AsmcRun e0 = asmc_run_begin(s, psi);
       for (int k = 0; k < 10; ++k) asmc_substep_f32(s, a0, a1, x, y, psi, u, v, r, xl, yl, pl, kt, ps + k, pert);
-      x += xl; y += yl; psi += pl;
+      asmc_run_end(x, y, psi, xl, yl, pl, e0, s);
     } else {
       for (int k = 0; k < 10; ++k) asmc_substep<R>(s, a0, a1, x, y, psi, u, v, r, ps + k, pert);
     }
@@ -647,8 +653,9 @@ __device__ __forceinline__ void asmc_env_chain(const State<R>& S, int e, int el0
     // perturb_step of the episode's UsvAsmc: 2 compute() x 10 substeps per env step (usv_asmc.py:199)
     const bool pert = S.perturb != 0;
     if constexpr (std::is_same<R, float>::value) {
-      float xl = 0.0f, yl = 0.0f, pl = 0.0f;        // position increments, heading compensation (asmc_substep_f32)
+      float xl = 0.0f, yl = 0.0f, pl = 0.0f;        // position sums, heading compensation (asmc_substep_f32)
       const float kt = rintf(psi * 0.159154943f);    // whole turns of the heading (asmc_substep_f32's J)
+      const AsmcRun e0 = asmc_run_begin(s, psi);    // eta_dot_last and psi before the run (asmc_run_end)
       // perturbation hoisted out of the substep loop, so the common loop unrolls (by 4): no
       // loop-carried register rotation (the s[1..3], s[4..9] moves) and the scheduler fills one
       // substep's hazard nops with the next one's independent work (dyn_rec_kernel 13.6 -> 11.4 us
@@ -659,7 +666,7 @@ __device__ __forceinline__ void asmc_env_chain(const State<R>& S, int e, int el0
 #pragma unroll 4
         for (int k = 0; k < 20; ++k) asmc_substep_f32(s, c0, c1, x, y, psi, u, v, r, xl, yl, pl, kt, 0, false);
       }
-      x += xl; y += yl; psi += pl;
+      asmc_run_end(x, y, psi, xl, yl, pl, e0, s);
     } else {
       if (pert) {
         for (int k = 0; k < 20; ++k) asmc_substep<R>(s, c0, c1, x, y, psi, u, v, r, 20 * el0 + k, true);
@@ -3512,7 +3519,7 @@ int usv_create(const usv_config* cfg, int32_t device, void** out) {
     // at 65 536 envs: 40.3 us, against 47.7 for the split dyn_kernel + scan), else 8
     h->kind = 3; h->epb = cfg->num_envs >= 49152 ? 64 : 32;
   } else { h->kind = 1; h->epb = 64; }
-  h->prio = h->kind >= 4 ? 0 : 1;      // the ramp helps static splits only
+  h->prio = h->kind >= 4 ? 0 : USV_STATIC_PRIO;   // the ramp helps static splits only
   if (const int rc = queue_lds_attr(h); rc != USV_OK) { delete h; return rc; }
   const int rc = cfg->precision == USV_F32 ? carve<float>(h, h->sf) : carve<double>(h, h->sd);
   if (rc != USV_OK) {
@@ -3552,7 +3559,7 @@ int usv_set_kernel_variant(void* hp, int32_t kind, int32_t epb, int32_t lid) {
   h->kind = kind;
   h->epb = epb;
   h->lid = lid;
-  h->prio = kind >= 4 ? 0 : 1;
+  h->prio = kind >= 4 ? 0 : USV_STATIC_PRIO;
   h->sf.prio = h->sd.prio = h->prio;
   h->sf.rowspan = h->sd.rowspan = rs ? rs == 0x100 : h->cfg.num_envs >= kRowSpanFrom;
   return USV_OK;
