@@ -16,6 +16,8 @@ for i in 1 2; do
 done
 bash tools/profile_round.sh r05b > $O/prof_r05b.log 2>&1
 rc=$?; echo "prof rc $rc"; stop $rc
+ENV_ID=usv-asmc-simple KERNELS="usv::(step_q_kernel|asmc_chain_kernel)" bash tools/profile_round.sh r05b_asmc > $O/prof_r05b_asmc.log 2>&1
+rc=$?; echo "prof asmc rc $rc"; stop $rc
 timeout -k 10 300 python tools/done_rate.py > $O/done_rate.json 2>&1
 rc=$?; echo "done rate rc $rc"; stop $rc
 timeout -k 10 200 python tools/api_throughput.py --envs 4096 > $O/api_4096.json 2>&1
