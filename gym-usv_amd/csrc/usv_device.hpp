@@ -451,14 +451,15 @@ __device__ __forceinline__ void asmc_substep_f32(float (&s)[kAsmcN], float a0, f
   const float vmag = __builtin_amdgcn_sqrtf(fmaf(u, u, v * v));
   // yaw channel: LOS heading, third-order filter, sliding surface (:72-89, :119-121, :134)
   const float beta = asin_f32(v * __builtin_amdgcn_rcpf(0.001f + vmag));
-  const float psi_d = psi + beta + a1;
+  const float ba = beta + a1;                                                   // psi_d - psi (:119)
+  const float psi_d = psi + ba;
   const float r_d = (psi_d - s[0]) * float(1.0 / H);
   s[0] = psi_d;
   const float o_dd = 4.0f * ((r_d - s[1]) - s[2]);
   const float o_d = fmaf(o_dd + s[3], h2, s[2]);
   const float o = fmaf(o_d + s[2], h2, s[1]);
   s[1] = o; s[2] = o_d; s[3] = o_dd;
-  const float e_psi = asmc_wrap(psi_d - psi);
+  const float e_psi = asmc_wrap(ba);
   const float sig_p = (o - r) + float(LAMBDA_PSI) * e_psi;
   // surge channel (:128-133)
   const float e_u = a0 - u;
@@ -475,9 +476,11 @@ __device__ __forceinline__ void asmc_substep_f32(float (&s)[kAsmcN], float a0, f
                           s[14] * copysignf(__builtin_amdgcn_sqrtf(fabsf(sig_u)), sig_u)));   // lambda e - ua
   const float au_p = fmaf(float(K2_PSI), sig_p, fmaf(float(LAMBDA_PSI), e_psi,
                           s[15] * copysignf(__builtin_amdgcn_sqrtf(fabsf(sig_p)), sig_p)));
-  // J(psi_old) (:179), psi reduced by the env step's whole turns kt (see the round-4 note above)
-  const float pr = fmaf(kt, 1.74845553e-07f, fmaf(-kt, 6.28318548f, psi));
-  const float sp = __sinf(pr), cp = __cosf(pr);
+  // J(psi_old) (:179): v_sin / v_cos take revolutions; psi / 2 pi less the env step's whole turns kt
+  // (the round-4 note above) in one fma: its error, |psi| 3e-8 / 2 pi revolutions, stays below half
+  // an ulp of psi itself
+  const float rev = fmaf(psi, float(1.0 / (2 * kPi)), -kt);
+  const float sp = __builtin_amdgcn_sinf(rev), cp = __builtin_amdgcn_cosf(rev);
   float p0 = 0.0f, p1 = 0.0f;
   if (perturb) {                                                                // T += F @ J (:184-198)
     double fx, fy;
@@ -488,7 +491,7 @@ __device__ __forceinline__ void asmc_substep_f32(float (&s)[kAsmcN], float a0, f
   }
   const float xuu = au > 1.2f ? -70.92f : 0.0f;                                 // :95-99 (Xu cancels)
   const float qs = fmaf(xuu * au, 1.0f - u, fmaf(float(Y_R_DOT + N_V_DOT), r, float(Y_V_DOT) * v) * r);
-  const float ud = fmaf(float(MI00), p0 - qs, au_u);                            // :226
+  const float ud = perturb ? fmaf(float(MI00), p0 - qs, au_u) : fmaf(float(-MI00), qs, au_u);  // :226
   const float md11 = fmaf(float(YV_K + YVV), av, float(YVR) * ar);
   const float md12 = fmaf(float(YR_K), vmag, fmaf(float(YRV), av, float(YRR) * ar));
   const float md21 = fmaf(float(NV_K), vmag, fmaf(float(NVV), av, float(NVR) * ar));

@@ -28,12 +28,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--envs", type=int, default=65536)
     ap.add_argument("--warm", type=int, default=200)
+    ap.add_argument("--env-id", default="usv-simple")
     ap.add_argument("--variant", default=None, help="kernel variant epb,lid,kind (e.g. 128,263,5: row spans on)")
     args = ap.parse_args()
     import gym_usv_amd
     lib = gym_usv_amd.load_library()
     lib.usv_diag_qprof.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
-    env = gym_usv_amd.make_vec("usv-simple", args.envs, seed=1, kernel_variant=args.variant)
+    env = gym_usv_amd.make_vec(args.env_id, args.envs, seed=1, kernel_variant=args.variant)
     env.reset(seed=1)
     g = torch.Generator(device="cuda").manual_seed(0)
     lo, span = torch.tensor([0.2, -1.0], device="cuda"), torch.tensor([0.8, 2.0], device="cuda")
@@ -52,7 +53,7 @@ def main():
     q = buf.reshape(16384, 12)[:nw].astype(np.float64)
     pairs, passes = q[:, 8], q[:, 9]
     life = sum(q[:, k] for k in NAMES)
-    out = {"event_us": round(e0.elapsed_time(e1) * 1e3, 2), "waves": nw,
+    out = {"env_id": args.env_id, "event_us": round(e0.elapsed_time(e1) * 1e3, 2), "waves": nw,
            "pairs_per_wave": [float(pairs.mean()), float(pairs.min()), float(pairs.max())],
            "passes_per_pair": float(passes.sum() / pairs.sum()),
            "life_cycles_mean": float(life.mean()), "life_cycles_p90": float(np.percentile(life, 90))}
