@@ -391,10 +391,11 @@ __device__ __forceinline__ void asmc_substep(R (&s)[kAsmcN], R a0, R a1, R& x, R
 //  * trapezoids H (a + b) / 2 + c as one fma by H / 2; ((r_d - o) F1 - F3 o') F2 with F = 2 as
 //    4 ((r_d - o) - o') (:86; bit-identical); np.sign products as copysign.
 //  * a ~50 m float position rounded at each of the 20 substeps was the f32 path's largest error (the
-//    reward's ye term amplifies it), so the position is rounded once per env step: x and y are not
-//    read inside the substep, so xl, yl accumulate their increments and the caller adds them after the
-//    20 substeps; psi is read by the next substep, so it integrates with compensated summation (pl
-//    carries what each addition rounded away; golden replay reward error 1.0e-4 -> 3.5e-5).
+//    reward's ye term amplifies it), so the pose is rounded once per run of substeps: x and y are not
+//    read inside the substep, so they accumulate in xl, yl and the caller applies them after the run;
+//    psi is read by the next substep, so it also integrates as usual and pl carries the correction
+//    (round 3, v1: the increments, with psi's compensated summation; golden replay reward error
+//    1.0e-4 -> 3.5e-5; round 5, v2: the rates, telescoped below).
 // End of a run of f32 substeps: the pose from what asmc_substep_f32 accumulated.  Round 5: xl, yl, pl
 // are the sums of the rates x', y', r over the run, and each trapezoid sum is telescoped,
 // sum_k h2 (q_k + q_{k-1}) = h2 (2 sum - q_last + q_{-1}) (q_{-1} = s[4], s[5], s[6] before the run:
