@@ -19,6 +19,10 @@ import torch
 from . import _lib
 from .spaces import Box
 
+# storage use count (a private torch binding): a copy=True output set is reused only when its storage
+# has no view outside the env; without the binding every copy=True step allocates a fresh set
+_STORAGE_USE_COUNT = getattr(torch._C, "_storage_Use_Count", None)
+
 ENV_SPECS = {
     # id: (mode, max_episode_steps)  -- gym_usv/__init__.py:3-34
     "usv-simple": (_lib.MODE_SIMPLE, 500),
@@ -306,10 +310,11 @@ class UsvVectorEnv:
         Work queued on other streams that reads a dropped output must record that stream on it, as
         for any tensor the caching allocator may reuse."""
         ring = self.__dict__.setdefault("_out_ring", [])
-        for ent in ring:
+        use_count = _STORAGE_USE_COUNT
+        for ent in ring if use_count is not None else ():
             ts, st, base_use, ptrs = ent
             if sys.getrefcount(ts) <= 3 and all(sys.getrefcount(t) <= 3 for t in ts if t is not None) and \
-                    torch._C._storage_Use_Count(st._cdata) == base_use:
+                    use_count(st._cdata) == base_use:
                 return ts, ptrs
         n, d, dev = self.num_envs, self.obs_dim, self.device
         rb = torch.empty((), dtype=self._rdt).element_size()
@@ -328,7 +333,7 @@ class UsvVectorEnv:
         del rew_b, info_bytes, obs_b, fobs_b, flags
         st = buf.untyped_storage()
         del buf
-        base_use = torch._C._storage_Use_Count(st._cdata)
+        base_use = use_count(st._cdata) if use_count is not None else None
         ptrs = (_ptr(obs), _ptr(rew), _ptr(term), _ptr(trunc), _ptr(done), _ptr(fobs), _ptr(ib))
         if len(ring) >= self._RING:
             ring.pop(0)                                # (still the caller's if it holds it)

@@ -243,3 +243,29 @@ def test_copy_outputs_are_reused_only_when_unreferenced_cpu():
     del nxt, rew
     assert f._fresh_outputs()[0][0].data_ptr() != p_obs    # obs still held
     del obs
+
+
+def test_copy_outputs_without_storage_use_count_are_always_fresh_cpu(monkeypatch):
+    """Without torch's private storage use-count binding a copy=True step never reuses an output set
+    (vector_env._STORAGE_USE_COUNT = None): every call returns new storage."""
+    from gym_usv_amd import vector_env
+    from gym_usv_amd.vector_env import UsvVectorEnv
+
+    monkeypatch.setattr(vector_env, "_STORAGE_USE_COUNT", None)
+
+    class Fake:
+        _RING = UsvVectorEnv._RING
+        _fresh_outputs = UsvVectorEnv._fresh_outputs
+
+        def __init__(self):
+            self.num_envs, self.obs_dim, self.device = 4, 143, torch.device("cpu")
+            self._rdt, self.info_enabled = torch.float32, False
+
+    f = Fake()
+    for _ in range(5):
+        ts, _p = f._fresh_outputs()
+        assert ts[6] is None
+        del ts, _p
+    assert len(f._out_ring) <= UsvVectorEnv._RING
+    # (the allocator may hand a freed block back; what matters is that no set came from the ring)
+    assert all(ent[2] is None for ent in f._out_ring)
