@@ -1123,7 +1123,7 @@ __device__ __forceinline__ void lidar_window(float dx, float dy, float key, floa
 __device__ __forceinline__ void lidar_window2(float dx, float dy, float key, float d, float rr, bool valid, bool far,
                                               float c0r, float s0r, float4* rec, const WinLds& L, int* mark2,
                                               Scan<float>& A, Scan<float>& B, QProf* qp = nullptr,
-                                              int rotA = 0, int rotB = 0) {
+                                              int rotA = 0, int rotB = 0, int* wout = nullptr) {
   const int l = lane_id();
   float a, b;
   to_ray0(dx, dy, c0r, s0r, a, b);
@@ -1147,6 +1147,7 @@ __device__ __forceinline__ void lidar_window2(float dx, float dy, float key, flo
   const int incl = wave_incl_scan(cnt);
   const int off = wave_excl_of(incl);
   const int W = __builtin_amdgcn_readlane(incl, 63);
+  if (wout) *wout = W;                                 // (diagnostic builds: the pair's window size)
   // Segment marks: obstacle lane l's run of pairs starts at off and maps pair q to slot
   // q + (lo - off) + 128 [env B], i.e. ray (slot & 127).  Its mark, written at off, is
   // l << 16 | (lo - off + 128 [env B] + 32768): the owner in the high bits keeps the max-scan in
@@ -1252,7 +1253,7 @@ __device__ __forceinline__ void lidar_window2(float dx, float dy, float key, flo
 __device__ __forceinline__ void lidar_wave2(float* rows, int os, int nl, float px, float py, float c0r,
                                             float s0r, const float2* rayoff, unsigned long long* slot,
                                             int* mark, int* mark2, Scan<float>& A, Scan<float>& B,
-                                            QProf* qp = nullptr, int rotA = 0, int rotB = 0) {
+                                            QProf* qp = nullptr, int rotA = 0, int rotB = 0, int* wout = nullptr) {
   const int l = lane_id();
   const int jl = l & 31;
   const bool valid = jl < nl;
@@ -1271,7 +1272,7 @@ __device__ __forceinline__ void lidar_wave2(float* rows, int os, int nl, float p
   A.far = B.far = false;
   const bool far = (vm & ballot(d >= (float)(0.99 * kSensorMax))) != 0;
   lidar_window2(dx, dy, key, d, rr, valid, far, c0r, s0r, reinterpret_cast<float4*>(rows), WinLds{slot, mark, rayoff},
-                mark2, A, B, qp, rotA, rotB);
+                mark2, A, B, qp, rotA, rotB, wout);
 }
 
 // Angular-window lidar for the f64 build (one env per wave).  The ray windows are sized in float from
@@ -2207,6 +2208,9 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
   // same-step autoresets of a pair run outside the pair loop (the loop is left and re-entered):
   // inside it their registers would spill the loop's to scratch
   int it = 0;
+#ifdef USV_DIAG_STAMPS
+  unsigned wsum = 0;                                   // (diagnostic: window sizes of this wave's pairs)
+#endif
   const bool hb = l >= 32;
   auto pair_hasb = [&](int p) { return 2 * p + 1 < nbe; };
   const float* const oblk = S.orow(eb);               // this block's obstacle rows (pair p at 2 p rowb bytes)
@@ -2288,8 +2292,15 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
       const int rotA = span2 ? kHdr + sh : 0, rotB = span2 ? 2 * kHdr + sh : 0;
       Scan<float> sa, sb;
       QMARK(1);
+#ifdef USV_DIAG_STAMPS
+      int wq = 0;
+      lidar_wave2(cbuf, os, (hb && !hasB) ? 0 : (nt & 0xffff), pose.x, pose.y, pose.z, pose.w, rayoff, slot,
+                  mark, reinterpret_cast<int*>(nbuf) + 192, sa, sb, qp, rotA, rotB, &wq);
+      wsum += (unsigned)wq;
+#else
       lidar_wave2(cbuf, os, (hb && !hasB) ? 0 : (nt & 0xffff), pose.x, pose.y, pose.z, pose.w, rayoff, slot,
                   mark, reinterpret_cast<int*>(nbuf) + 192, sa, sb, qp, rotA, rotB);
+#endif
       float4 pose_n = pose, meta_n = meta;
       float hv_n = hv;
       if (nxt >= 0) rec_of(nxt, pose_n, meta_n, hv_n);   // the next pair's record (wave-uniform)
@@ -2378,7 +2389,9 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
   }
   QMARK(11);
   qprof_flush(qp);
-  USV_STAMP_V(4, (unsigned long long)it);            // (diagnostic: pairs this wave scanned)
+#ifdef USV_DIAG_STAMPS
+  USV_STAMP_V(4, (unsigned long long)it | ((unsigned long long)wsum << 16));   // (pairs | window sizes << 16)
+#endif
   USV_STAMP_W(3);
   USV_STAMP_W(6);
 }

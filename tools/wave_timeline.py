@@ -145,8 +145,23 @@ def main():
         out["slowest_cus"] = [[int(cus[i]), round(float(cs[i]), 2),
                                [round(x[1] - x[0], 2) for x in sorted(per_cu[cus[i]])],
                                round(float(ce[i]), 2)] for i in slow]
-        pairs_w = raw[:, 4].astype(np.int64)
+        pairs_w = (raw[:, 4] & 0xFFFF).astype(np.int64)
+        wsum_w = (raw[:, 4] >> 16).astype(np.int64)      # window sizes of the wave's pairs (work)
         out["pairs_per_wave"] = pct(pairs_w)
+        # is the CU-to-CU spread work?  per CU: the window sizes its waves scanned against its busy time
+        cw = np.array([wsum_w[np.isin(blk_id, [x[2] for x in per_cu[c]])].sum() for c in cus], dtype=np.float64)
+        if cw.std() > 0:
+            busy = ce - cs
+            out["cu_work_windows"] = pct(cw)
+            out["corr_cu_work_busy"] = round(float(np.corrcoef(cw, busy)[0, 1]), 3)
+            out["corr_cu_work_end"] = round(float(np.corrcoef(cw, ce)[0, 1]), 3)
+            slope = np.polyfit(cw, busy, 1)
+            out["cu_busy_us_per_1000_windows"] = round(float(slope[0] * 1000), 3)
+            resid = busy - np.polyval(slope, cw)
+            out["cu_busy_residual_us"] = pct(resid)
+            bw = np.array([wsum_w[blk_id == b].sum() for b in range(nb)], dtype=np.float64)
+            be = np.array([float(st[blk_id == b, 4].max() - st[blk_id == b, 0].min()) for b in range(nb)])
+            out["corr_block_work_busy"] = round(float(np.corrcoef(bw, be)[0, 1]), 3)
         # per role (older / younger block of a CU): phase-1 end (stamp 1), barrier exit (2), end (6),
         # pairs scanned per wave
         role = np.zeros(nw, np.int64)
