@@ -3,6 +3,11 @@
     python bench.py [--gpus N] [--steps K] [--warmup W] [--envs 65536] [--env-id usv-simple]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
+--gpus N without a launcher starts N rank processes itself (spawn_ranks: fresh interpreters, the
+same environment torch.distributed.run gives its ranks); under a launcher --gpus must equal
+WORLD_SIZE, and --gpus beyond the visible GPUs is refused (resolve_world), so an N-GPU line is
+always N ranks on N GPUs.
+
 A "step" is one launch of the fused step kernel over every env of the rank (config C3:
 usv-simple, 65 536 envs, random actions in [0.2,1]x[-1,1], in-kernel TimeLimit + same-step
 autoreset).  Actions for all K timed steps are generated on the device before the timed
@@ -264,10 +269,15 @@ def f64_leg(args, N, rank, dev, stream, acts, pool):
                     "the contract; traffic from profiles/pmc_summary.json"}
 
 
-# --------------------------------------------------------------------------- main
-def main():
+# --------------------------------------------------------------------------- launch
+BACKEND = "nccl"            # RCCL on ROCm; tests/test_multirank.py runs the same ranks under gloo
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks, one per GPU: under torch.distributed.run it must equal WORLD_SIZE; "
+                         "without a launcher N > 1 starts N rank processes itself")
     ap.add_argument("--steps", type=int, default=10000)
     ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--envs", type=int, default=65536, help="envs per GPU")
@@ -290,68 +300,217 @@ def main():
                     help="launches of the f64 (reference-precision) leg after the timed region (0 = skip)")
     ap.add_argument("--api-steps", type=int, default=200, help="steps of the public-API leg (0 = skip)")
     ap.add_argument("--variant", default=None, help="step-kernel variant epb,lid,kind (tools; default: tuned)")
-    args = ap.parse_args()
+    return ap.parse_args(argv)
 
+
+def resolve_world(gpus, environ, device_count):
+    """How this process takes part, from --gpus and the launcher's environment:
+      ("rank", world)  -- this process is one rank: WORLD_SIZE set by torch.distributed.run (or by
+                          spawn_ranks) and equal to --gpus, or a plain single-GPU run;
+      ("spawn", gpus)  -- --gpus N > 1 with no launcher: start N rank processes (spawn_ranks).
+    Refuses (SystemExit with a message, exit status 1) a WORLD_SIZE that differs from --gpus, and
+    --gpus N beyond the visible GPUs, so an N-GPU line is never measured on fewer GPUs.
+    `device_count` is called only in the spawn case (torch.cuda.device_count() does not initialise
+    the GPU, so the parent stays GPU-free before it starts its children)."""
+    if gpus < 1:
+        raise SystemExit(f"bench.py: --gpus must be >= 1, got {gpus}")
+    ws = environ.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != gpus:
+            raise SystemExit(f"bench.py: --gpus {gpus} but the launcher started WORLD_SIZE={ws} ranks; "
+                             f"pass --gpus {ws} (or --nproc-per-node {gpus})")
+        return "rank", int(ws)
+    if gpus == 1:
+        return "rank", 1
+    have = int(device_count())
+    if have < gpus:
+        raise SystemExit(f"bench.py: --gpus {gpus} needs {gpus} visible GPUs, this node shows {have}; "
+                         "refusing to report a smaller run as an N-GPU one")
+    return "spawn", gpus
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _rank_entry(rank, world, port, argv):
+    """Body of one spawned rank: the environment torch.distributed.run would give it, then main()."""
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      USV_BENCH_LAUNCHER="bench.py spawn")
+    main(argv)
+
+
+def spawn_ranks(n, argv, target=_rank_entry, port=None):
+    """Start n rank processes (multiprocessing "spawn": fresh interpreters, nothing forked from or
+    exec'd over this process, which has made no GPU call) and wait for them.  Returns 0, or the exit
+    status of the first rank that fails, after terminating the others (a rank left waiting in a
+    barrier for a dead peer would otherwise hang)."""
+    from multiprocessing.connection import wait
+    ctx = mp.get_context("spawn")
+    port = port or _free_port()
+    procs = [ctx.Process(target=target, args=(r, n, port, list(argv)), name=f"bench-rank{r}") for r in range(n)]
+    for p in procs:
+        p.start()
+    rc, live = 0, list(procs)
+    while live:
+        wait([p.sentinel for p in live])
+        for p in [p for p in live if not p.is_alive()]:
+            p.join()
+            live.remove(p)
+            if p.exitcode != 0 and rc == 0:
+                rc = p.exitcode if p.exitcode > 0 else 1
+                print(f"bench.py: {p.name} exited with status {p.exitcode}; stopping the other ranks",
+                      file=sys.stderr, flush=True)
+                for q in live:
+                    q.terminate()
+    return rc
+
+
+def init_dist(local):
+    """One process group over the ranks (BACKEND); the NCCL (RCCL) group is bound to this rank's GPU."""
     import torch
     import torch.distributed as dist
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    if BACKEND == "nccl":
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
-    torch.cuda.set_device(dev)
+    else:
+        dist.init_process_group(BACKEND)
 
-    import gym_usv_amd
-    N, K, W = args.envs, args.steps, args.warmup
-    env = gym_usv_amd.make_vec(args.env_id, N, device=local, seed=args.seed, precision=args.precision,
-                               lidar=args.lidar, env_id_offset=shard(rank, N)[0], kernel_variant=args.variant)
-    env.reset(seed=args.seed)
-    mean_obs = float(env.get_field("n_obs").mean())
-    A, D = env.act_dim, env.obs_dim
 
-    # actions for every timed step resident in HBM before timing (cycled pool if huge)
-    pool = max(1, min(K, (8 << 30) // (N * 4 * A)))
-    gen = torch.Generator(device=dev).manual_seed(args.seed * 7919 + rank)
-    if A == 2:
-        lo, span = torch.tensor([0.2, -1.0], device=dev), torch.tensor([0.8, 2.0], device=dev)
-    else:                                       # legacy heading offset (usv_asmc_env.py:74-75)
-        lo, span = torch.tensor([-math.pi / 2], device=dev), torch.tensor([math.pi], device=dev)
-    acts = torch.rand((pool, N, A), device=dev, generator=gen) * span + lo
-    obs = torch.empty((N, D), device=dev)
-    fobs = torch.empty((N, D), device=dev)
-    rew = torch.empty(N, device=dev, dtype=torch.float32 if args.precision == "f32" else torch.float64)
-    term = torch.empty(N, device=dev, dtype=torch.uint8)
-    trunc = torch.empty(N, device=dev, dtype=torch.uint8)
-    stream = torch.cuda.current_stream(dev)
-    sptr = stream.cuda_stream
+# --------------------------------------------------------------------------- the timed workload
+class _StreamEvent:
+    """A HIP event recorded on the env's stream (torch.cuda.Event sees only what it is recorded on)."""
 
-    # the C-ABI call with its arguments bound once per action buffer (usv_step, include/usv_hip.h):
-    # the host path of a launch is one ctypes call
-    import ctypes
-    step_fn = env.lib.usv_step
-    vp = ctypes.c_void_p
-    outs = (vp(obs.data_ptr()), vp(rew.data_ptr()), vp(term.data_ptr()), vp(trunc.data_ptr()), vp(fobs.data_ptr()),
-            vp(sptr))
-    bound = [(env._h, vp(acts[i].data_ptr())) + outs for i in range(pool)]
+    def __init__(self, stream):
+        import torch
+        self.e, self.s = torch.cuda.Event(enable_timing=True), stream
 
-    def launch(k):
-        rc = step_fn(*bound[k % pool])
+    def record(self):
+        self.e.record(self.s)
+
+    def elapsed_time(self, other):
+        return self.e.elapsed_time(other.e)
+
+    def synchronize(self):
+        self.e.synchronize()
+
+
+class StepWorkload:
+    """Config C3 on one rank: the vector env over this rank's shard of global env ids, the actions of
+    every timed step resident in HBM, and the C-ABI step call with its arguments bound once per action
+    buffer (usv_step, include/usv_hip.h), so the host path of a launch is one ctypes call."""
+
+    def __init__(self, args, rank, local):
+        import ctypes
+        import torch
+        import gym_usv_amd
+        self.args, self.rank = args, rank
+        dev = self.dev = torch.device("cuda", local)
+        torch.cuda.set_device(dev)
+        self.collective_device = dev
+        N = self.N = args.envs
+        env = self.env = gym_usv_amd.make_vec(args.env_id, N, device=local, seed=args.seed,
+                                              precision=args.precision, lidar=args.lidar,
+                                              env_id_offset=shard(rank, N)[0], kernel_variant=args.variant)
+        env.reset(seed=args.seed)
+        self.mean_obs = float(env.get_field("n_obs").mean())
+        A, D = env.act_dim, env.obs_dim
+        # actions for every timed step resident in HBM before timing (cycled pool if huge)
+        pool = self.pool = max(1, min(args.steps, (8 << 30) // (N * 4 * A)))
+        gen = torch.Generator(device=dev).manual_seed(args.seed * 7919 + rank)
+        if A == 2:
+            lo, span = torch.tensor([0.2, -1.0], device=dev), torch.tensor([0.8, 2.0], device=dev)
+        else:                                   # legacy heading offset (usv_asmc_env.py:74-75)
+            lo, span = torch.tensor([-math.pi / 2], device=dev), torch.tensor([math.pi], device=dev)
+        self.acts = torch.rand((pool, N, A), device=dev, generator=gen) * span + lo
+        self.obs = torch.empty((N, D), device=dev)
+        self.fobs = torch.empty((N, D), device=dev)
+        self.rew = torch.empty(N, device=dev, dtype=torch.float32 if args.precision == "f32" else torch.float64)
+        self.term = torch.empty(N, device=dev, dtype=torch.uint8)
+        self.trunc = torch.empty(N, device=dev, dtype=torch.uint8)
+        self.stream = torch.cuda.current_stream(dev)
+        vp = ctypes.c_void_p
+        outs = (vp(self.obs.data_ptr()), vp(self.rew.data_ptr()), vp(self.term.data_ptr()),
+                vp(self.trunc.data_ptr()), vp(self.fobs.data_ptr()), vp(self.stream.cuda_stream))
+        self.bound = [(env._h, vp(self.acts[i].data_ptr())) + outs for i in range(pool)]
+        self.step_fn = env.lib.usv_step
+
+    def launch(self, k):
+        rc = self.step_fn(*self.bound[k % self.pool])
         if rc != 0:
-            raise RuntimeError(env.lib.usv_last_error().decode())
+            raise RuntimeError(self.env.lib.usv_last_error().decode())
+
+    def sync(self):
+        import torch
+        torch.cuda.synchronize(self.dev)
+
+    def event(self):
+        return _StreamEvent(self.stream)
+
+    def extras(self):
+        """The legs after the timed region, untimed by the contract: the f64 (reference-precision)
+        kernel and the public-API step."""
+        import torch
+        args, env, N, pool, acts = self.args, self.env, self.N, self.pool, self.acts
+        # the reference's precision (float64, simple_env.py:32-54) on the same workload: its own env
+        # and the same launch path, one event pair around --f64-steps launches
+        f64 = None
+        if args.f64_steps > 0 and args.precision == "f32" and args.env_id not in LEGACY_IDS:
+            f64 = f64_leg(args, N, self.rank, self.dev, self.stream, acts, pool)
+        # public API leg: UsvVectorEnv.step on the same envs
+        api = None
+        if args.api_steps > 0:
+            api = {}
+            for copy in (True, False):
+                env.copy = copy
+                for k in range(8):
+                    env.step(acts[k % pool])
+                torch.cuda.synchronize(self.dev)
+                t1 = time.perf_counter()
+                for k in range(args.api_steps):
+                    env.step(acts[k % pool])
+                torch.cuda.synchronize(self.dev)
+                dt = (time.perf_counter() - t1) / args.api_steps
+                api["copy" if copy else "nocopy"] = {"env_steps_per_s": round(N / dt, 1),
+                                                     "us_per_step": round(dt * 1e6, 2)}
+            api["steps"] = args.api_steps
+            api["note"] = ("UsvVectorEnv.step(actions) -> (obs, reward, terminated, truncated, info) with "
+                           "torch tensors on the device; copy=True returns fresh tensors (gymnasium default), "
+                           "copy=False the persistent buffers")
+        return {"f64": f64, "api_step": api}
+
+    def close(self):
+        self.env.close()
+
+
+# --------------------------------------------------------------------------- main
+def run(args, rank, world, local, workload_cls=None):
+    """One rank of the bench: warm-up, the timed window, the kernel timing, the max over ranks; rank 0
+    returns (and prints) the JSON line, the other ranks return None."""
+    import torch.distributed as dist
+    if world > 1:
+        init_dist(local)
+    ranks_seen = dist.get_world_size() if dist.is_available() and dist.is_initialized() else 1
+    wl = (workload_cls or StepWorkload)(args, rank, local)
+    N, K, W = wl.N, args.steps, args.warmup
+    launch = wl.launch
 
     for k in range(W):
         launch(k)
     # clock warm-up (untimed): keep stepping until the GPU has been busy for --clock-warmup seconds
-    torch.cuda.synchronize(dev)
+    wl.sync()
     extra, tw = 0, time.perf_counter()
     while time.perf_counter() - tw < args.clock_warmup:
         for _ in range(64):
             launch(W + extra)
             extra += 1
-        torch.cuda.synchronize(dev)
+        wl.sync()
     W2 = W + extra
     # HIP events on the env's stream bracket groups of G back-to-back launches (one event pair
     # per group; a pair around every single launch would add its own gap to each launch)
@@ -359,30 +518,29 @@ def main():
     G = max(1, args.event_every)
     edge = args.event_layout == "edge"
     groups = 1 if edge else (K - 1) // G
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(groups)]
+    ev = [(wl.event(), wl.event()) for _ in range(groups)]
     for a, b in ev:                                   # the events exist before the timed region
-        a.record(stream)
-        b.record(stream)
+        a.record()
+        b.record()
 
     def timed_launch(k):
         if edge:
             # one timing marker before the first launch and one after the last: a marker between two
             # launches makes the second wait for the first's end-of-kernel release (tools/probe_wall.py)
             if k == 0:
-                ev[0][0].record(stream)
+                ev[0][0].record()
             launch(W2 + k)
             if k == K - 1:
-                ev[0][1].record(stream)
+                ev[0][1].record()
             return
         g, r = divmod(k - 1, G)
         if k > 0 and g < groups and r == 0:
-            ev[g][0].record(stream)
+            ev[g][0].record()
         launch(W2 + k)
         if k > 0 and g < groups and r == G - 1:
-            ev[g][1].record(stream)
+            ev[g][1].record()
 
-    t0, t1 = timed_window(timed_launch, K, lambda: torch.cuda.synchronize(dev),
-                          dist.barrier if world > 1 else (lambda: None))
+    t0, t1 = timed_window(timed_launch, K, wl.sync, dist.barrier if world > 1 else (lambda: None))
     elapsed = t1 - t0
     if edge:
         kern_ms = ev[0][0].elapsed_time(ev[0][1]) / K
@@ -393,44 +551,20 @@ def main():
     # 16-launch group when the driver runs --steps 20
     steady_ms = None
     if args.steady_steps > 0:
-        sa, sb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        sa.record(stream)
+        sa, sb = wl.event(), wl.event()
+        sa.record()
         for k in range(args.steady_steps):
             launch(W2 + K + k)
-        sb.record(stream)
+        sb.record()
         sb.synchronize()
         steady_ms = sa.elapsed_time(sb) / args.steady_steps
-    elapsed, kern_ms, steady_ms = reduce_max([elapsed, kern_ms, steady_ms or 0.0], device=dev)
+    elapsed, kern_ms, steady_ms = reduce_max([elapsed, kern_ms, steady_ms or 0.0], device=wl.collective_device)
+    legs = wl.extras()
 
-    # the reference's precision (float64, simple_env.py:32-54) on the same workload, untimed by the
-    # contract: its own env and the same launch path, one event pair around --f64-steps launches
-    f64 = None
-    if args.f64_steps > 0 and args.precision == "f32" and args.env_id not in LEGACY_IDS:
-        f64 = f64_leg(args, N, rank, dev, stream, acts, pool)
-
-    # public API leg (untimed by the contract above): UsvVectorEnv.step on the same envs
-    api = None
-    if args.api_steps > 0:
-        api = {}
-        for copy in (True, False):
-            env.copy = copy
-            for k in range(8):
-                env.step(acts[k % pool])
-            torch.cuda.synchronize(dev)
-            t1 = time.perf_counter()
-            for k in range(args.api_steps):
-                env.step(acts[k % pool])
-            torch.cuda.synchronize(dev)
-            dt = (time.perf_counter() - t1) / args.api_steps
-            api["copy" if copy else "nocopy"] = {"env_steps_per_s": round(N / dt, 1), "us_per_step": round(dt * 1e6, 2)}
-        api["steps"] = args.api_steps
-        api["note"] = ("UsvVectorEnv.step(actions) -> (obs, reward, terminated, truncated, info) with torch "
-                       "tensors on the device; copy=True returns fresh tensors (gymnasium default), copy=False "
-                       "the persistent buffers")
-
+    out = None
     if rank == 0:
         value = aggregate_rate(N, world, K, elapsed)
-        bpe = algorithmic_bytes_per_env_step(args.env_id, mean_obs, args.precision)
+        bpe = algorithmic_bytes_per_env_step(args.env_id, wl.mean_obs, args.precision)
         bytes_per_launch = bpe * N
         achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
         traffic, valu = pmc_entry(args.pmc, f"{args.env_id}/{N}/{args.precision}/{args.lidar}")
@@ -440,13 +574,15 @@ def main():
         out = {
             "metric": METRIC, "value": round(value, 1), "unit": "env-steps/s", "n_gpus": world,
             "steps": K, "warmup": W, "clock_warmup_steps": extra, "ms_per_step": round(elapsed / K * 1e3, 5),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "ranks_seen": world,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "ranks_seen": ranks_seen,
+            "launcher": os.environ.get("USV_BENCH_LAUNCHER",
+                                       "torch.distributed.run" if world > 1 else "single process"),
             "dtype": args.precision, "data": "synthetic (on-device uniform random actions, Philox env resets)",
             "config": {"workload": f"C3: {args.env_id}, {N} envs per GPU, random-action rollout, "
                                    f"in-kernel TimeLimit + same-step autoreset",
                        "env_id": args.env_id, "envs_per_gpu": N, "global_envs": N * world,
                        "parallelism": f"env-sharded x{world}, no step-path collective",
-                       "lidar": args.lidar, "mean_obstacles": round(mean_obs, 2)},
+                       "lidar": args.lidar, "mean_obstacles": round(wl.mean_obs, 2)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic, "kernel_ms": round(kern_ms, 5),
@@ -460,8 +596,8 @@ def main():
                                                "after the timed region"} if steady_ms else None),
                          "valu_basis": "SQ_INSTS_VALU per launch (profiles/pmc_summary.json) x 2 cycles / "
                                        "(1024 SIMDs x 2.4 GHz x kernel_ms)" if valu_frac is not None else None},
-            "api_step": api,
-            "f64": f64,
+            "api_step": legs["api_step"],
+            "f64": legs["f64"],
         }
         if args.env_id in LEGACY_IDS:
             out["config"].pop("lidar")
@@ -472,9 +608,25 @@ def main():
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
-    env.close()
+    wl.close()
     if world > 1:
         dist.destroy_process_group()
+    return out
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
+    args = parse_args(argv)
+
+    def device_count():
+        import torch
+        return torch.cuda.device_count()
+    mode, world = resolve_world(args.gpus, os.environ, device_count)
+    if mode == "spawn":
+        sys.exit(spawn_ranks(world, argv))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    run(args, rank, world, local)
 
 
 if __name__ == "__main__":
