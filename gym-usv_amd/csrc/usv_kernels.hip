@@ -2140,6 +2140,8 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
   // (a wave's loads return in issue order); the barrier below publishes them.
   constexpr int kDynWaves = FUSED ? (kQE + kWave - 1) / kWave : 0;
   static_assert(kQW >= 3 * kDynWaves + 1 && 2 * kQW <= kQE + 2 * kWave, "block shape");
+  // the store flags qdyn[0..kDynWaves-1] live in the 16-B qctr words (lds_q_bytes), before qnob
+  static_assert(kDynWaves <= 2, "qdyn holds two dynamics waves' flags");
   if (wave >= kDynWaves && cur >= 0) dma_copy1(S.orow(eb + 2 * cur), rowbuf0, min(2, nbe - 2 * cur) * rowb);
   if (FUSED && wave >= kDynWaves && wave < 2 * kDynWaves) {
     const int w = wave - kDynWaves;
@@ -2198,7 +2200,7 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
   // cost 0.5 / 1.8 us, draining before the barrier 0.05 / 1.6 us; gpurun_out r5h, r5i).
   if (FUSED && wave < kDynWaves) {
     vm_wait<0>();
-    qdyn[wave] = 1u;
+    __hip_atomic_store(qdyn + wave, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
 #endif
   USV_STAMP_W(2);
@@ -2380,7 +2382,7 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
         // the env's phase-1 stores (by dynamics wave (e - eb) / 64) are acknowledged before its reset
         // stores are issued: two waves' stores to one address are otherwise unordered
         const unsigned* const f = qdyn + ((e - eb) >> 6);
-        while (__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
+        while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u)
           __builtin_amdgcn_s_sleep(2);
       }
       reset_wave<float, MODE>(S, e, io.obs + (size_t)e * kObsDim);
@@ -3444,11 +3446,20 @@ int usv_asmc_compute(int32_t precision, int32_t n, const void* act, void* pos, v
   if (n < 0 || calls < 0) return fail(USV_ERR_ARG, "n and calls must be >= 0");
   if (n == 0 || calls == 0) return USV_OK;
   if (!act || !pos || !vel || !state) return fail(USV_ERR_ARG, "null argument");
-  // launch on the device that holds the state, whatever the caller's current device is
-  hipPointerAttribute_t pa{};
-  if (hipPointerGetAttributes(&pa, state) != hipSuccess || pa.device < 0)
-    return fail(USV_ERR_ARG, "state is not a device pointer");
-  DeviceGuard g(pa.device);
+  // launch on the device that holds the state, whatever the caller's current device is; every buffer
+  // must be device-accessible memory of that device (a pageable host pointer would fault the kernel)
+  auto device_of = [](const void* p) {
+    hipPointerAttribute_t pa{};
+    return hipPointerGetAttributes(&pa, p) == hipSuccess ? pa.device : -1;
+  };
+  const int dev = device_of(state);
+  if (dev < 0) { (void)hipGetLastError(); return fail(USV_ERR_ARG, "state is not a device pointer"); }
+  if (device_of(act) != dev || device_of(pos) != dev || device_of(vel) != dev ||
+      (perturb_step && device_of(perturb_step) != dev)) {
+    (void)hipGetLastError();
+    return fail(USV_ERR_ARG, "act / pos / vel / perturb_step are not device pointers on the state's device");
+  }
+  DeviceGuard g(dev);
   const dim3 grid((n + kBlock - 1) / kBlock), block(kBlock);
   hipStream_t st = (hipStream_t)stream;
   if (precision == USV_F32)

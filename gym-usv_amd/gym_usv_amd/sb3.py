@@ -30,10 +30,12 @@ the small arrays (reward, done) first, and the terminal rows of the done envs on
 arrays alternate between two such buffer sets, so each stays valid until the second-next step
 (SB3's collectors consume or copy them within one step).  ``infos`` is a new list every step; a done
 env's info is a new dict; an env that did not end gets an empty dict that is reused across steps
-only while it stays empty: a dict a wrapper or callback wrote into is replaced by a new one before
-the next step (one C-level ``any()`` over the list detects it), so no write ever shows up in a
-later step's infos -- what DummyVecEnv's fresh dicts guarantee -- without building 4096 dicts per
-step (~0.1-0.2 ms of Python).
+only while it stays empty: a dict a wrapper or callback wrote into BEFORE the next ``step_wait`` is
+replaced by a new one there (one C-level ``any()`` over the list detects it), so such a write never
+shows up in a later step's infos, without building 4096 dicts per step (~0.1-0.2 ms of Python).
+A write into step t's empty dict made AFTER step t+1 has returned (a consumer that keeps infos lists
+and annotates them later) does show up in step t+1's infos, which DummyVecEnv's fresh dicts never
+do: pass ``fresh_infos=True`` for a new dict per env and step, as DummyVecEnv builds them.
 The env's device is the current device for the whole call (events and copies are ordered on its
 stream even when another device is current in the caller).
 """
@@ -100,7 +102,8 @@ class Sb3VecEnv:
     ``num_envs``, ``obs_dim``, ``act_dim``, ``single_*_space``, ``reset(seed=)``, ``step()`` with
     same-step autoreset and ``info["final_obs"]``)."""
 
-    def __init__(self, env_id="usv-simple", num_envs=4096, frame_stack=0, seed=0, venv=None, **kw):
+    def __init__(self, env_id="usv-simple", num_envs=4096, frame_stack=0, seed=0, venv=None,
+                 fresh_infos=False, **kw):
         if venv is None:
             from .vector_env import UsvVectorEnv
             # each step is consumed (copied to the host) before the next: the persistent buffers do
@@ -136,6 +139,7 @@ class Sb3VecEnv:
         self._act_dev = torch.empty((n, venv.act_dim), dtype=torch.float32, device=dev)
         self._rew32 = torch.empty(n, dtype=torch.float32, device=dev)
         self._copy_stream = torch.cuda.Stream(dev) if self._cuda else None
+        self._fresh_infos = bool(fresh_infos)
         self._infos = [{} for _ in range(n)]            # per env: empty unless it ended this step
         self._filled = np.empty(0, dtype=np.int64)
 
@@ -201,13 +205,16 @@ class Sb3VecEnv:
             h["obs"].copy_(obs)
             h["rew"].copy_(rew)
             h["done"].copy_(done)
-        infos = self._infos
-        for i in self._filled:                          # last step's done envs: new empty dicts
-            infos[i] = {}
-        if any(infos):                                  # a consumer wrote into an empty info dict:
-            for i, d in enumerate(infos):               # replace it (theirs keeps the write)
-                if d:
-                    infos[i] = {}
+        if self._fresh_infos:                           # DummyVecEnv: a new dict per env and step
+            infos = self._infos = [{} for _ in range(n)]
+        else:
+            infos = self._infos
+            for i in self._filled:                      # last step's done envs: new empty dicts
+                infos[i] = {}
+            if any(infos):                              # a consumer wrote into an empty info dict:
+                for i, d in enumerate(infos):           # replace it (theirs keeps the write)
+                    if d:
+                        infos[i] = {}
         done_np = h["done"].numpy()
         idx = np.flatnonzero(done_np)
         if idx.size:

@@ -77,6 +77,53 @@ def _ptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
 
 
+class _OutSet:
+    """A copy=True output set (UsvVectorEnv._fresh_outputs): the tensors, their storage, ctypes
+    pointers, the reference-state baseline, and whether a tensor of it was recorded on a stream."""
+    __slots__ = ("ts", "st", "ptrs", "base", "exposed", "__weakref__")
+
+    @classmethod
+    def make(cls, n, d, dev, rdt, info_enabled):
+        import weakref
+        ent = cls()
+        rb = torch.empty((), dtype=rdt).element_size()
+        ob = n * d * 4
+        info_b = n * _lib.INFO_DIM * rb if info_enabled else 0
+        # byte layout: rewards and info rows first (8-B aligned), then obs, final obs, the flags
+        sizes = (n * rb, info_b, ob, ob, 3 * n)
+        buf = torch.empty(sum(sizes), dtype=torch.uint8, device=dev)
+        rew_b, info_bytes, obs_b, fobs_b, flags = buf.split(sizes)
+        term, trunc, done = flags.view(torch.bool).view(3, n).unbind(0)
+        ent.ts = (obs_b.view(torch.float32).view(n, d), rew_b.view(rdt), term, trunc, done,
+                  fobs_b.view(torch.float32).view(n, d),
+                  info_bytes.view(rdt).view(n, _lib.INFO_DIM) if info_enabled else None)
+        ent.st = buf.untyped_storage()
+        ent.ptrs = tuple(_ptr(t) for t in ent.ts)
+        ent.base, ent.exposed = None, False
+        wself = weakref.ref(ent)
+        for t in ent.ts:
+            if t is not None:
+                # the tensor's record_stream, which also retires the set from the ring (instance
+                # attribute: it shadows Tensor.record_stream for this tensor only; weak references,
+                # so neither the tensor nor the set gains a reference)
+                t.record_stream = _retiring_record_stream(weakref.ref(t), wself)
+        return ent
+
+    def state(self):
+        ts = self.ts
+        return (sys.getrefcount(ts), tuple(sys.getrefcount(t) for t in ts if t is not None),
+                tuple(t._use_count() for t in ts if t is not None), _STORAGE_USE_COUNT(self.st._cdata))
+
+
+def _retiring_record_stream(wt, wset):
+    def record_stream(stream):
+        s = wset()
+        if s is not None:
+            s.exposed = True
+        return torch.Tensor.record_stream(wt(), stream)
+    return record_stream
+
+
 class UsvVectorEnv:
     """``num_envs`` USV path-following envs on one GPU.
 
@@ -303,42 +350,31 @@ class UsvVectorEnv:
     def _fresh_outputs(self):
         """One output set of a copy=True step: (obs, reward, terminated, truncated, done, final_obs,
         info rows) and their ctypes pointers.  A set is one device allocation viewed as the outputs;
-        a set returned earlier is handed out again only when nothing outside this env refers to it
-        any more -- none of its tensor objects is referenced elsewhere and its storage has no other
-        view -- so the caller always gets tensors that alias nothing it holds (gymnasium's copy=True),
-        at the cost of two reference-count reads instead of five caching-allocator calls per step.
-        Work queued on other streams that reads a dropped output must record that stream on it, as
-        for any tensor the caching allocator may reuse."""
+        a set returned earlier is handed out again only when nothing outside this env can still read
+        it, i.e. its reference state is back at the baseline taken when it was made (_OutSet.state):
+          * no Python reference to the tuple or to one of its tensors (sys.getrefcount, read by the
+            same code at creation and at reuse, so the interpreter's own counting cancels out);
+          * no other view of the storage (the storage use count);
+          * no C++ holder of a tensor (TensorImpl use count: a DLPack capsule, an autograd graph);
+          * no other stream recorded on a tensor: ``record_stream`` on a handed-out tensor retires its
+            set from the ring for good, so the caching allocator frees it only after that stream's
+            work, exactly as for any tensor it owns.
+        Otherwise a new set is allocated: the caller always gets tensors that alias nothing it holds
+        or still reads (gymnasium's copy=True), at the cost of a few reference-count reads instead of
+        an allocation and seven views per step."""
         ring = self.__dict__.setdefault("_out_ring", [])
-        use_count = _STORAGE_USE_COUNT
-        for ent in ring if use_count is not None else ():
-            ts, st, base_use, ptrs = ent
-            if sys.getrefcount(ts) <= 3 and all(sys.getrefcount(t) <= 3 for t in ts if t is not None) and \
-                    use_count(st._cdata) == base_use:
-                return ts, ptrs
-        n, d, dev = self.num_envs, self.obs_dim, self.device
-        rb = torch.empty((), dtype=self._rdt).element_size()
-        ob = n * d * 4
-        info_b = n * _lib.INFO_DIM * rb if self.info_enabled else 0
-        # byte layout: rewards and info rows first (8-B aligned), then obs, final obs, the flags
-        sizes = (n * rb, info_b, ob, ob, 3 * n)
-        buf = torch.empty(sum(sizes), dtype=torch.uint8, device=dev)
-        rew_b, info_bytes, obs_b, fobs_b, flags = buf.split(sizes)
-        rew = rew_b.view(self._rdt)
-        ib = info_bytes.view(self._rdt).view(n, _lib.INFO_DIM) if self.info_enabled else None
-        obs = obs_b.view(torch.float32).view(n, d)
-        fobs = fobs_b.view(torch.float32).view(n, d)
-        term, trunc, done = flags.view(torch.bool).view(3, n).unbind(0)
-        ts = (obs, rew, term, trunc, done, fobs, ib)
-        del rew_b, info_bytes, obs_b, fobs_b, flags
-        st = buf.untyped_storage()
-        del buf
-        base_use = use_count(st._cdata) if use_count is not None else None
-        ptrs = (_ptr(obs), _ptr(rew), _ptr(term), _ptr(trunc), _ptr(done), _ptr(fobs), _ptr(ib))
+        if _STORAGE_USE_COUNT is not None:
+            for ent in ring:
+                if not ent.exposed and ent.state() == ent.base:
+                    return ent.ts, ent.ptrs
+        ent = _OutSet.make(self.num_envs, self.obs_dim, self.device, self._rdt, self.info_enabled)
         if len(ring) >= self._RING:
             ring.pop(0)                                # (still the caller's if it holds it)
-        ring.append((ts, st, base_use, ptrs))
-        return ts, ptrs
+        ring.append(ent)
+        ring[:] = [e for e in ring if not e.exposed]   # retired sets: the allocator's from now on
+        if _STORAGE_USE_COUNT is not None:
+            ent.base = ent.state()
+        return ent.ts, ent.ptrs
 
     def step_raw(self, actions, obs, reward, term, trunc, final_obs=None, stream=None):
         """Launch one step into caller-owned buffers (no checks, no allocation): bench / graphs."""

@@ -255,7 +255,7 @@ int usv_step_ex(void* handle, const float* act_dev, float* obs_dev, void* rew_de
  *   perturb_step_dev int32 [n] or NULL (= 0): the controllers' perturb_step (:49), advanced by 10
  *     per call; do_perturb adds the sinusoidal disturbance (:184-199).
  * Stream-ordered, no handle (ABI v5); launched on the device that holds state_dev, whatever device is
- * current (USV_ERR_ARG if state_dev is not a device pointer). */
+ * current (USV_ERR_ARG if any buffer is not device memory of the device that holds state_dev). */
 int usv_asmc_compute(int32_t precision, int32_t n, const void* act_dev, void* pos_dev, void* vel_dev,
                      void* state_dev, int32_t* perturb_step_dev, int32_t do_perturb, int32_t calls,
                      void* stream);

@@ -70,6 +70,7 @@ def test_asmc_highspeed_replay(golden, precision, perturb, fixture):
     flips = rays = 0
     worst_entry = -1
     cont = np.array([k for k in range(16) if k not in (11, 12)])    # continuous state entries
+    rows = np.zeros(16)                         # per state row: max relative error
     band = idx % 3                              # gen_asmc_highspeed: |psi| <= pi, <= 30, 300..400 rad
     bw = {b: dict(hdr=0.0, rew=0.0, flips=0) for b in range(3)}
     for t in range(T):
@@ -91,6 +92,7 @@ def test_asmc_highspeed_replay(golden, precision, perturb, fixture):
             worst["vel"] = max(worst["vel"], float((np.abs(ivel[m] - rv) / np.maximum(1, np.abs(rv))).max()))
             worst["pos"] = max(worst["pos"], float((np.abs(ipos[m] - rp) / np.maximum(1, np.abs(rp))).max()))
             d = np.abs(st[m][:, cont] - rs[m][:, cont]) / np.maximum(1, np.abs(rs[m][:, cont]))
+            rows[cont] = np.maximum(rows[cont], d.max(axis=0))
             if float(d.max()) > worst["state"]:
                 worst["state"] = float(d.max())
                 worst_entry = int(cont[np.unravel_index(np.argmax(d), d.shape)[1]])
@@ -109,7 +111,8 @@ def test_asmc_highspeed_replay(golden, precision, perturb, fixture):
           f"Ka-switch flips {int(flipped.sum())}/{n} envs (rate {flipped.mean():.3f}); "
           + ", ".join(f"{k} {v:.2e}" for k, v in worst.items()) + f" (state row {worst_entry})"
           + f"; sensor flips {flips}/{rays}; by |psi| band "
-          + "; ".join(f"{b}: hdr {v['hdr']:.2e} rew {v['rew']:.2e} flips {v['flips']}" for b, v in bw.items()))
+          + "; ".join(f"{b}: hdr {v['hdr']:.2e} rew {v['rew']:.2e} flips {v['flips']}" for b, v in bw.items())
+          + "; state rows " + " ".join(f"{k}:{rows[k]:.1e}" for k in cont))
     assert fast > 0 and (orc.asmc.fast_substeps > 0).sum() >= n // 3
     assert flipped.sum() <= (0 if precision == "f64" else HS_FLIPS.get((fixture, perturb), max(2, n // 8))), \
         flipped.sum()
@@ -138,15 +141,23 @@ def test_reference_asmc_tests_on_hip(golden, precision):
     g = golden("asmc_compute.npz")
     worst = 0.0
     band = {}
-    for name, act in (("kat_zero", [0, 0]), ("kat_fwd", [10, 0]), ("kat_rot", [0, 10])):
-        asmc = UsvAsmc(precision=precision)
+    def run(prec, act):
+        asmc = UsvAsmc(precision=prec)
         position, velocity = np.zeros(3), np.zeros(3)
         traj = []
         for k in range(1000):
             position, velocity, _ = asmc.compute(np.array(act, dtype=np.float64), position, velocity, False)
             if k < 50 or k % 50 == 49:
                 traj.append(np.concatenate([position, velocity]))
-        traj = np.stack(traj)
+        return position, velocity, np.stack(traj)
+    vs64 = None
+    for name, act in (("kat_zero", [0, 0]), ("kat_fwd", [10, 0]), ("kat_rot", [0, 10])):
+        position, velocity, traj = run(precision, act)
+        if name == "kat_rot" and precision == "f32":
+            # the f32 controller against this library's own f64 one on the same calls: f64 follows
+            # the reference to 5.7e-15 over the first 300 calls, so this tracks the f32 arithmetic alone
+            t64 = run("f64", act)[2]
+            vs64 = float((np.abs(traj - t64) / np.maximum(1, np.abs(t64)))[:, [2, 3, 5]].max())
         if name == "kat_zero":                                       # test_no_movement :8-16
             assert np.allclose(position, np.zeros(3)) and np.allclose(velocity, np.zeros(3))
         elif name == "kat_fwd":                                      # test_forward_movement :18-28
@@ -166,7 +177,8 @@ def test_reference_asmc_tests_on_hip(golden, precision):
             late = late[:, [2, 3, 5]]
         band[name] = float(late.max())
         print(f"\n[KAT {name} {precision}] final pos {position}, vel {velocity}; ref final {ref[-1]}; "
-              f"first 300 calls max rel err {err.max():.2e}; calls 350-1000 band {band[name]:.2e}")
+              f"first 300 calls max rel err {err.max():.2e}; calls 350-1000 band {band[name]:.2e}"
+              + (f"; f32 vs own f64 (psi, u, r) over 1000 calls {vs64:.2e}" if name == "kat_rot" and vs64 is not None else ""))
     # measured: f64 5.7e-15, f32 4.4e-5 (kat_rot)
     assert worst <= (3e-14 if precision == "f64" else 2.5e-4), worst
     # calls 350-1000, measured (round 5): see KAT_BAND

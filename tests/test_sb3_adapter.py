@@ -122,6 +122,28 @@ def test_sb3_infos_are_fresh_each_step_cpu():
         assert len(ids) == fv.num_envs                     # no dict shared between envs
 
 
+def test_sb3_fresh_infos_deferred_writes_cpu():
+    """Default: a write into step t's empty info dict made after step t+1 returned shows up in step
+    t+1's infos (documented); fresh_infos=True builds new dicts per env and step, as DummyVecEnv, so a
+    deferred write never leaks."""
+    for fresh in (False, True):
+        fv = FakeVenv(T=10)
+        env = Sb3VecEnv(venv=fv, fresh_infos=fresh)
+        env.reset()
+        kept = []
+        for t in range(10):
+            _, _, dn, infos = env.step(np.zeros((fv.num_envs, 2), np.float32))
+            if kept:
+                for d in kept[-1]:
+                    d["annotated_later"] = t          # deferred annotation of the previous step's infos
+            leaked = [i for i, d in enumerate(infos) if "annotated_later" in d]
+            if fresh:
+                assert leaked == [], (t, leaked)
+            kept.append(infos)
+        if not fresh:
+            assert any("annotated_later" in d for d in kept[-1])   # the documented aliasing
+
+
 def test_device_frame_stack_no_final_obs_cpu():
     fs = DeviceFrameStack(3, 2, 3, torch.device("cpu"))
     fs.reset(torch.ones(3, 2))
@@ -268,4 +290,45 @@ def test_copy_outputs_without_storage_use_count_are_always_fresh_cpu(monkeypatch
         del ts, _p
     assert len(f._out_ring) <= UsvVectorEnv._RING
     # (the allocator may hand a freed block back; what matters is that no set came from the ring)
-    assert all(ent[2] is None for ent in f._out_ring)
+    assert all(ent.base is None for ent in f._out_ring)
+
+
+def test_copy_outputs_held_by_dlpack_or_recorded_on_a_stream_are_not_reused_cpu():
+    """A copy=True set exported through DLPack (a C++ holder: no Python reference, no storage view)
+    is not handed out again while the capsule lives; a set one of whose tensors was passed to
+    record_stream is retired from the ring for good (vector_env._OutSet)."""
+    from torch.utils import dlpack
+    from gym_usv_amd.vector_env import UsvVectorEnv
+
+    class Fake:
+        _RING = UsvVectorEnv._RING
+        _fresh_outputs = UsvVectorEnv._fresh_outputs
+
+        def __init__(self):
+            self.num_envs, self.obs_dim, self.device = 8, 143, torch.device("cpu")
+            self._rdt, self.info_enabled = torch.float32, False
+
+    f = Fake()
+    ts, _ = f._fresh_outputs()
+    p = ts[0].data_ptr()
+    cap = dlpack.to_dlpack(ts[1])              # the reward tensor, exported
+    del ts, _
+    ts2, _ = f._fresh_outputs()
+    assert ts2[0].data_ptr() != p              # the capsule still holds the first set
+    del ts2, _
+    del cap
+    ts3, _ = f._fresh_outputs()
+    assert ts3[0].data_ptr() == p              # capsule gone: reusable again
+    try:
+        ts3[0].record_stream(None)             # (a CPU tensor has no stream: the call itself may fail)
+    except Exception:
+        pass
+    ring = f._out_ring
+    assert any(e.exposed for e in ring)
+    del ts3, _
+    held = []
+    for _ in range(4):                         # the recorded set never comes back from the ring
+        ts4, _ = f._fresh_outputs()
+        assert not any(e.exposed and e.ts is ts4 for e in f._out_ring)
+        held.append(ts4)
+    assert not any(e.exposed for e in f._out_ring)   # retired: dropped at the next allocation
