@@ -109,9 +109,9 @@ class _OutSet:
                 t.record_stream = _retiring_record_stream(weakref.ref(t), wself)
         return ent
 
-    def state(self):
+    def state(self, own=()):
         ts = self.ts
-        return (sys.getrefcount(ts), tuple(sys.getrefcount(t) for t in ts if t is not None),
+        return (sys.getrefcount(ts), tuple(sys.getrefcount(t) - own.count(id(t)) for t in ts if t is not None),
                 tuple(t._use_count() for t in ts if t is not None), _STORAGE_USE_COUNT(self.st._cdata))
 
 
@@ -364,8 +364,12 @@ class UsvVectorEnv:
         an allocation and seven views per step."""
         ring = self.__dict__.setdefault("_out_ring", [])
         if _STORAGE_USE_COUNT is not None:
+            # the env's own references to the last step's outputs (reset(mask=) keeps the rows of the
+            # envs it does not reset) are not the caller's: ids, so that reading them adds none
+            d = self.__dict__
+            own = (id(d.get("_last_obs")), id(d.get("_last_rew")), id(d.get("info_buf")))
             for ent in ring:
-                if not ent.exposed and ent.state() == ent.base:
+                if not ent.exposed and ent.state(own) == ent.base:
                     return ent.ts, ent.ptrs
         ent = _OutSet.make(self.num_envs, self.obs_dim, self.device, self._rdt, self.info_enabled)
         if len(ring) >= self._RING:

@@ -31,15 +31,26 @@ def to_np(*ts):
     return [t.detach().cpu().numpy() for t in ts]
 
 
-# Bounds ~5x the worst case measured on the round-4 tree (printed by the test; profiles/r04_gpu_errors.txt),
+# (Round 4 / 5 history.)  Bounds ~5x the worst case measured on the round-4 tree (printed by the test; profiles/r04_gpu_errors.txt),
 # capped by SURVEY 8(c) where that is tighter.  f64 measured: obs header exact, reward 3.6e-15, pose /
 # velocity 2.5e-16, ASMC state 1.8e-13 (OCML's exp / asin / sin / cos against glibc's differ in the last
 # bit, and 20 substeps carry it); f32: header 7.1e-6 (8(c) 1e-5), reward 3.5e-5 (8(c) 1e-4), pose /
 # velocity 3.5e-5 relative, state 1.6e-3.
 # Round 5 (240-env fixture, 5x more envs): f64 reward 4.0e-14, state 6.2e-13; f32 state 7.4e-3 (row 7,
 # the surge acceleration u_dot_last, relative to max(1, |ref|)) -- bounds raised to ~5x / ~3x those.
-HS_TOL = {"f64": dict(hdr=0.0, rew=2e-13, vel=2e-15, state=3e-12),
-          "f32": dict(hdr=1e-5, rew=1e-4, vel=1.5e-4, state=2.5e-2)}
+# Round 6: the ASMC state bound is per row (verdict r5 #4): 2x the largest error each row
+# showed over both fixtures and both modes (round-6 tree, gpurun_out/r6a; the test prints every row).
+# Rows (usv_hip.h usv_asmc_compute): 0 psi_d_last, 1-3 the heading filter o, o', o'', 4-6 eta_dot_last,
+# 7-9 upsilon_dot_last (the surge / sway / yaw accelerations, which jump with every Ka-switch-adjacent
+# rounding), 10 e_u_last, 13 e_u_int, 14-15 Ka_u, Ka_psi (11, 12 are the switches: counted as flips).
+# Measured f32 maxima: 2.3e-4 2.2e-4 1.1e-3 3.6e-3 | 6.1e-4 1.3e-3 2.1e-4 | 7.4e-3 5.6e-4 1.5e-3 |
+# 3.2e-4 6.7e-5 2.5e-3 6.4e-6 (rows 7 and 3 from the perturbed 240-env half).
+HS_STATE_ROWS_F32 = {0: 5e-4, 1: 5e-4, 2: 2.5e-3, 3: 7.5e-3, 4: 1.5e-3, 5: 3e-3, 6: 5e-4,
+                     7: 1.5e-2, 8: 1.5e-3, 9: 3e-3, 10: 7e-4, 13: 1.5e-4, 14: 5e-3, 15: 1.5e-5}
+# measured (round 6): f64 reward 4.0e-14, state 6.2e-13 (row 3), velocity 4.4e-16, position 1.1e-15;
+# f32 header 7.9e-6, reward 3.5e-5, velocity 6.3e-6, position 5.7e-5
+HS_TOL = {"f64": dict(hdr=0.0, rew=8e-14, vel=1e-15, pos=2.5e-15, state=1.2e-12),
+          "f32": dict(hdr=1e-5, rew=7e-5, vel=1.5e-5, pos=1e-4, state=None)}
 
 
 # f32 envs whose Ka switch lands on the other branch (the round-5 240-env fixture gives the rate
@@ -118,7 +129,12 @@ def test_asmc_highspeed_replay(golden, precision, perturb, fixture):
         flipped.sum()
     tol = HS_TOL[precision]
     assert worst["hdr"] <= tol["hdr"] and worst["rew"] <= tol["rew"], worst
-    assert worst["vel"] <= tol["vel"] and worst["pos"] <= tol["vel"] and worst["state"] <= tol["state"], worst
+    assert worst["vel"] <= tol["vel"] and worst["pos"] <= tol["pos"], worst
+    if precision == "f64":
+        assert worst["state"] <= tol["state"], worst
+    else:
+        over = {k: (float(rows[k]), b) for k, b in HS_STATE_ROWS_F32.items() if rows[k] > b}
+        assert not over, f"ASMC state rows over their bounds: {over}"
     assert flips <= (0 if precision == "f64" else max(2, rays // 10000))
     env.close()
 
@@ -127,8 +143,13 @@ def test_asmc_highspeed_replay(golden, precision, perturb, fixture):
 # calls 350..1000 of the reference KATs (round 5; measured in parentheses): kat_fwd stays smooth
 # (f64 5.2e-15, f32 1.9e-5); kat_rot's heading-rate switching makes even f64 drift (9.3e-2 on psi,
 # u, r at call 1000), f32 8.6e-2 -- a band around the reference trajectory, not a tolerance
-KAT_BAND = {"f64": {"kat_zero": 0.0, "kat_fwd": 3e-14, "kat_rot": 0.2},
-            "f32": {"kat_zero": 0.0, "kat_fwd": 1e-4, "kat_rot": 0.25}}
+# Round 6: ~1.5x the measured values -- f64 kat_fwd 5.2e-15, kat_rot 9.25e-2; f32 kat_fwd
+# 1.85e-5, kat_rot 7.3e-2 (8.6-10.8 % across round 5's substep edits).  The f32 kat_rot trajectory against
+# this library's own f64 one drifts as far (8.3e-2 over 1000 calls): the switching, not the reference, sets
+# the band, so it is bounded the same way (KAT_ROT_VS_F64).
+KAT_BAND = {"f64": {"kat_zero": 0.0, "kat_fwd": 8e-15, "kat_rot": 0.14},
+            "f32": {"kat_zero": 0.0, "kat_fwd": 3e-5, "kat_rot": 0.12}}
+KAT_ROT_VS_F64 = 0.13
 
 
 @pytest.mark.parametrize("precision", ["f64", "f32"])
@@ -179,8 +200,10 @@ def test_reference_asmc_tests_on_hip(golden, precision):
         print(f"\n[KAT {name} {precision}] final pos {position}, vel {velocity}; ref final {ref[-1]}; "
               f"first 300 calls max rel err {err.max():.2e}; calls 350-1000 band {band[name]:.2e}"
               + (f"; f32 vs own f64 (psi, u, r) over 1000 calls {vs64:.2e}" if name == "kat_rot" and vs64 is not None else ""))
-    # measured: f64 5.7e-15, f32 4.4e-5 (kat_rot)
-    assert worst <= (3e-14 if precision == "f64" else 2.5e-4), worst
+    # measured: f64 5.7e-15, f32 4.5e-5 (kat_rot)
+    assert worst <= (9e-15 if precision == "f64" else 7e-5), worst
+    if vs64 is not None:
+        assert vs64 <= KAT_ROT_VS_F64, vs64
     # calls 350-1000, measured (round 5): see KAT_BAND
     for name, lim in KAT_BAND[precision].items():
         assert band[name] <= lim, (name, band[name])

@@ -332,3 +332,37 @@ def test_copy_outputs_held_by_dlpack_or_recorded_on_a_stream_are_not_reused_cpu(
         assert not any(e.exposed and e.ts is ts4 for e in f._out_ring)
         held.append(ts4)
     assert not any(e.exposed for e in f._out_ring)   # retired: dropped at the next allocation
+
+
+def test_copy_outputs_reused_while_the_env_keeps_its_last_obs_cpu():
+    """step() keeps its own references to the latest obs / reward / info rows (_last_obs, _last_rew,
+    info_buf, for reset(mask=)); those do not count as the caller's: a set the caller dropped comes
+    back although the env still refers to it, and a set the caller holds does not."""
+    from gym_usv_amd.vector_env import UsvVectorEnv
+
+    class Fake:
+        _RING = UsvVectorEnv._RING
+        _fresh_outputs = UsvVectorEnv._fresh_outputs
+
+        def __init__(self):
+            self.num_envs, self.obs_dim, self.device = 8, 143, torch.device("cpu")
+            self._rdt, self.info_enabled = torch.float32, True
+            self.info_buf = None
+
+        def step(self):
+            ts, _ = self._fresh_outputs()
+            self._last_obs, self._last_rew, self.info_buf = ts[0], ts[1], ts[6]
+            return ts[0], ts[1], ts[2], ts[3], {"final_obs": ts[5], "_final_obs": ts[4]}
+
+    f = Fake()
+    out = f.step()
+    p0 = out[0].data_ptr()
+    del out
+    out = f.step()                              # dropped by the caller, still env._last_obs
+    assert out[0].data_ptr() == p0
+    kept = out
+    out = f.step()
+    assert out[0].data_ptr() != p0              # held by the caller
+    ring_ptrs = {e.ts[0].data_ptr() for e in f._out_ring}
+    del out, kept
+    assert f.step()[0].data_ptr() in ring_ptrs     # nothing held: a ring set, no allocation
