@@ -407,20 +407,12 @@ __device__ __forceinline__ AsmcRun asmc_run_begin(const float (&s)[kAsmcN], floa
 }
 __device__ __forceinline__ void asmc_run_end(float& x, float& y, float& psi, float xl, float yl, float pl,
                                              const AsmcRun& e0, const float (&s)[kAsmcN]) {
-#ifndef USV_ASMC_F32_V1
   constexpr float h2 = float(H / 2);
   x += h2 * (fmaf(2.0f, xl, -s[4]) + e0.x4);
   y += h2 * (fmaf(2.0f, yl, -s[5]) + e0.y5);
   psi = e0.psi0 + h2 * (fmaf(2.0f, pl, -s[6]) + e0.r6);
-#else
-  (void)e0; (void)s;
-  x += xl;
-  y += yl;
-  psi += pl;
-#endif
 }
 
-#ifndef USV_ASMC_F32_V1
 // asin on [-1, 1] for the f32 substep: |x| < 1/2 as s + s t P(t) with t = x^2, else
 // pi/2 - 2 asin(sqrt((1 - |x|) / 2)) with the same polynomial (Cephes asinf's minimax P, ~2.5e-7
 // relative); one hardware sqrt, both arms branch-free
@@ -517,88 +509,5 @@ __device__ __forceinline__ void asmc_substep_f32(float (&s)[kAsmcN], float a0, f
   }
   s[4] = xd; s[5] = yd; s[6] = r;
 }
-#else
-__device__ __forceinline__ void asmc_substep_f32(float (&s)[kAsmcN], float a0, float a1, float& x, float& y,
-                                                 float& psi, float& u, float& v, float& r, float& xl, float& yl,
-                                                 float& pl, float kt, int pstep = 0, bool perturb = false) {
-  constexpr float h2 = float(H / 2);
-  const float au = fabsf(u), av = fabsf(v), ar = fabsf(r);
-  const float vmag = __builtin_amdgcn_sqrtf(fmaf(u, u, v * v));
-  // yaw channel: LOS heading, third-order filter, sliding surface (:72-89, :119-121, :134)
-  const float beta = asinf(v * __builtin_amdgcn_rcpf(0.001f + vmag));
-  const float psi_d = psi + beta + a1;
-  const float r_d = (psi_d - s[0]) * float(1.0 / H);
-  s[0] = psi_d;
-  const float o_dd = 4.0f * ((r_d - s[1]) - s[2]);
-  const float o_d = fmaf(o_dd + s[3], h2, s[2]);
-  const float o = fmaf(o_d + s[2], h2, s[1]);
-  s[1] = o; s[2] = o_d; s[3] = o_dd;
-  const float e_psi = asmc_wrap(psi_d - psi);
-  const float sig_p = (o - r) + float(LAMBDA_PSI) * e_psi;
-  // surge channel (:128-133)
-  const float e_u = a0 - u;
-  s[13] = fmaf(e_u + s[10], h2, s[13]);
-  s[10] = e_u;
-  const float sig_u = fmaf(float(LAMBDA_U), s[13], e_u);
-  // adaptive gains (:137-146) and control laws (:150-151)
-  const float kdu = s[14] > float(KMIN_U) ? asmc_ksign(float(K_U), fabsf(sig_u) - float(MU_U)) : float(KMIN_U);
-  const float kdp = s[15] > float(KMIN_PSI) ? asmc_ksign(float(K_PSI), fabsf(sig_p) - float(MU_PSI)) : float(KMIN_PSI);
-  s[14] = fmaf(kdu + s[11], h2, s[14]);
-  s[15] = fmaf(kdp + s[12], h2, s[15]);
-  s[11] = kdu; s[12] = kdp;
-  const float ua_u = asmc_root(s[14], sig_u) - float(K2_U) * sig_u;
-  const float ua_p = asmc_root(s[15], sig_p) - float(K2_PSI) * sig_p;
-  // tau = (Tx, 0, Tz) (:113-176)
-  const bool fast = au > 1.2f;                                                  // :95-99
-  const float xu = fast ? 64.55f : -25.0f;
-  const float xuu = fast ? -70.92f : 0.0f;
-  const float xd_u = fmaf(xuu, au, xu * u);                                     // Xuu |u| + Xu u
-  const float tx = fmaf(float(MASS - X_U_DOT), fmaf(float(LAMBDA_U), e_u, -ua_u),
-                        -fmaf(float(MASS - Y_V_DOT) * v, r, xd_u));
-  const float tz = fmaf(float(IZ - N_R_DOT), fmaf(float(LAMBDA_PSI), e_psi, -ua_p),
-                        -fmaf(float(-X_U_DOT + Y_V_DOT) * u, v, float(NR_K) * vmag * r));
-  // rhs = tau - C(nu) nu - D(nu) nu
-  const float c02 = fmaf(float(-MASS + 2 * Y_V_DOT), v, float(Y_R_DOT + N_V_DOT) * r);
-  const float c12 = float(MASS - X_U_DOT * MASS) * u;
-  const float d00 = fmaf(-xuu, au, -xu);
-  const float md11 = fmaf(float(YV_K + YVV), av, float(YVR) * ar);              // -d11
-  const float md12 = fmaf(float(YR_K), vmag, fmaf(float(YRV), av, float(YRR) * ar));
-  const float md21 = fmaf(float(NV_K), vmag, fmaf(float(NVV), av, float(NVR) * ar));
-  const float md22 = fmaf(float(NR_K), vmag, fmaf(float(NRV), av, float(NRR) * ar));
-  // J(psi_old) (:179): psi reduced by the env step's whole turns kt (reduce_2pi's two-constant step with
-  // k fixed for the 20 substeps: psi moves well under a turn in one env step, so the reduced argument
-  // stays within about half a turn of zero, where v_sin / v_cos are accurate)
-  const float pr = fmaf(kt, 1.74845553e-07f, fmaf(-kt, 6.28318548f, psi));
-  const float sp = __sinf(pr), cp = __cosf(pr);
-  float tt0 = tx, tt1 = 0.0f;
-  if (perturb) {                                                                // T += F @ J (:184-198)
-    double fx, fy;
-    perturb_force(pstep, fx, fy);
-    const float pfx = float(fx), pfy = float(fy);
-    tt0 = tx + (pfx * cp + pfy * sp);
-    tt1 = pfx * -sp + pfy * cp;
-  }
-  const float rhs0 = fmaf(-c02, r, fmaf(-d00, u, tt0));
-  const float rhs1 = fmaf(md11, v, fmaf(md12 - c12, r, tt1));
-  const float rhs2 = fmaf(c02, u, fmaf(c12 + md21, v, fmaf(md22, r, tz)));
-  const float ud = float(MI00) * rhs0;                                          // :226
-  const float vd = fmaf(float(MI11), rhs1, float(MI12) * rhs2);
-  const float rd = fmaf(float(MI21), rhs1, float(MI22) * rhs2);
-  u = fmaf(ud + s[7], h2, u);                                                   // :228-229
-  v = fmaf(vd + s[8], h2, v);
-  r = fmaf(rd + s[9], h2, r);
-  s[7] = ud; s[8] = vd; s[9] = rd;
-  const float xd = fmaf(cp, u, -(sp * v)), yd = fmaf(sp, u, cp * v);          // :233
-  {                                                                             // :234
-    const float ix = (xd + s[4]) * h2, iy = (yd + s[5]) * h2, ip = (r + s[6]) * h2;
-    xl += ix;                                                                   // x, y: added by the caller
-    yl += iy;
-    const float sq = psi + ip;
-    pl += ip - (sq - psi);                                                      // fast two-sum error
-    psi = sq;
-  }
-  s[4] = xd; s[5] = yd; s[6] = r;
-}
-#endif
 
 }  // namespace usv

@@ -170,14 +170,8 @@ __device__ __forceinline__ void qprof_flush(QProf*) {}
 template <typename T> __device__ __forceinline__ void st_out(T* p, T v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // global_store ... sc1
 }
-// obs-row stores of the block-queue step (diagnostic builds: -DUSV_OBS_PLAIN for plain stores)
-template <typename T> __device__ __forceinline__ void st_obs(T* p, T v) {
-#ifdef USV_OBS_PLAIN
-  *p = v;
-#else
-  st_out(p, v);
-#endif
-}
+// obs-row stores of the block-queue step: write-through like st_out
+template <typename T> __device__ __forceinline__ void st_obs(T* p, T v) { st_out(p, v); }
 
 // Obs-row store layout of the block-queue step (State::rowspan; usv_set_kernel_variant lid bits 0x100 /
 // 0x200 force it on / off; a template switch, SPAN, of the 128-env fused kernels without info rows, as
@@ -188,17 +182,9 @@ template <typename T> __device__ __forceinline__ void st_obs(T* p, T v) {
 // 256 MB Infinity Cache the pieces are faster (65 536 envs: 19.2 vs 20.3 us), so the default switches
 // at kRowSpanFrom envs.
 constexpr int kRowSpanFrom = 196608;
-#ifndef USV_QFLAG
-#define USV_QFLAG 3   // block queue: same-step resets wait for the dynamics waves' store flag (0: diagnostic off)
-#endif
-#ifndef USV_STATIC_PRIO
 // issue-priority mode of the static-split kinds 1-3 (State::prio: 1 ramp, 2 last iteration first, 0 none);
 // kind 3 f64 at 65 536 envs, same box: 1 -> 40.5 us, 0 -> 43.2, 2 -> 43.2
-#define USV_STATIC_PRIO 1
-#endif
-#ifndef USV_F64_REC_SOA
-#define USV_F64_REC_SOA 1   // lidar_wave2_d's per-obstacle records as two 16-B planes (round 5; 0: one 32-B record)
-#endif
+constexpr int kStaticPrio = 1;
 
 // Division and square root of the per-step dynamics: in the f32 build the hardware reciprocal and
 // square root (1 ulp; the reference's float64 values are matched to SURVEY 8(c)'s tolerance), which
@@ -1210,14 +1196,9 @@ __device__ __forceinline__ void lidar_window2(float dx, float dy, float key, flo
     wave_incl_max2_asm(m0, m1);
     m1 = max(m1, __builtin_amdgcn_readlane(m0, 63));
     carry = __builtin_amdgcn_readlane(m1, 63);
-#ifdef USV_PAIR_SERIAL
-    pair(0, m0);
-    pair(kWave, m1);
-#else
     const PairIn p0 = pair_ld(0, m0), p1 = pair_ld(kWave, m1);
     pair_do(0, p0);
     pair_do(kWave, p1);
-#endif
     base = 2 * kWave;
     pass = 2;
   }
@@ -1391,18 +1372,13 @@ __device__ __forceinline__ void lidar_wave2_d(const double* rows, int os, int nl
   // mark: owner lane + 1 in the high bits, slot offset (env B: + 128) in the low bits
   const int mk0 = ((l + 1) << 16) | (lo - off + (l >= 32 ? 128 : 0) + 32768);
   const unsigned long long kq = (ord_key64(key) & ~63ull) | (unsigned long long)l;
-#if USV_F64_REC_SOA
   // per-obstacle record as two 16-B planes (a, b) [64] and (r^2, key | lane) [64]: lane l's halves at a
   // 16-B stride, so the stores and the owners' gathers are bank-conflict free (a 32-B record stride
-  // put lanes 4 apart on the same banks)
+  // put lanes 4 apart on the same banks; round 5)
   double2* const recA = reinterpret_cast<double2*>(rec);
   double2* const recB = recA + kWave;
   recA[l] = make_double2(a, b);
   recB[l] = make_double2(r2, __longlong_as_double((long long)kq));
-#else
-  // per-obstacle record (a, b, r^2, key | lane) in LDS: a pair reads its owner's with two ds_read_b128
-  rec[l] = make_double4(a, b, r2, __longlong_as_double((long long)kq));
-#endif
   const int mpass = cnt > 0 ? off >> 6 : -1;
   int carry = 0;
   for (int base = 0, pass = 0; base < W; base += kWave, ++pass) {   // wave-uniform pass count
@@ -1414,12 +1390,8 @@ __device__ __forceinline__ void lidar_wave2_d(const double* rows, int os, int nl
     const int q = base + l;
     const int jj = max((mk >> 16) - 1, 0);
     const int si = (q + (mk & 0xffff) - 32768) & 255;
-#if USV_F64_REC_SOA
     const double2 oa = recA[jj], ob = recB[jj];
     const double4 o = make_double4(oa.x, oa.y, ob.x, ob.y);   // owner's (a, b, r^2, key | lane)
-#else
-    const double4 o = rec[jj];                         // owner's (a, b, r^2, key | lane)
-#endif
     const unsigned long long jk = (unsigned long long)__double_as_longlong(o.w);
     const double2 cs = rayoff[si & 127];
     const double proj = m_fma(o.x, cs.x, o.y * cs.y);  // ray_pair's arithmetic
@@ -1436,12 +1408,8 @@ __device__ __forceinline__ void lidar_wave2_d(const double* rows, int os, int nl
   mark[l] = 0;
   // reading of the winner (reading_of's arithmetic, the winner's record from LDS)
   auto reading = [&](double c, double sn, unsigned long long v) {
-#if USV_F64_REC_SOA
     const double2 wa = recA[(int)(v & 63)], wb = recB[(int)(v & 63)];
     const double4 w = make_double4(wa.x, wa.y, wb.x, wb.y);
-#else
-    const double4 w = rec[(int)(v & 63)];
-#endif
     const double proj = m_fma(w.x, c, w.y * sn);
     const double perp = m_fma(w.x, sn, -(w.y * c));
     const double delta = m_fma(-perp, perp, w.z);
@@ -1869,11 +1837,9 @@ __global__ __launch_bounds__(kWave * WPB) void scan_kernel(State<R> S, IO<R> io)
 }
 
 // f64 scan compiled for more waves per SIMD (the uncapped f64 scan takes 141 VGPRs: 3 waves)
-#ifndef USV_F64_SCAN_WAVES
-#define USV_F64_SCAN_WAVES 4
-#endif
+constexpr int kF64ScanWaves = 4;
 template <typename R, int MODE, int EPW, int LID, int WPB>
-__global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(USV_F64_SCAN_WAVES, USV_F64_SCAN_WAVES)))
+__global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(kF64ScanWaves, kF64ScanWaves)))
 void scan_kernel_d(State<R> S, IO<R> io) { scan_body<R, MODE, EPW, LID, WPB>(S, io); }
 
 // ---- fused with block-wide dynamics (kind 3, f64 usv-simple): wave 0 of each 4-wave block runs
@@ -1949,7 +1915,7 @@ __device__ __forceinline__ void step_body_blockdyn(const State<R>& S, const IO<R
 }
 
 template <typename R, int MODE, int EPW, int LID>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(USV_F64_SCAN_WAVES, USV_F64_SCAN_WAVES)))
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kF64ScanWaves, kF64ScanWaves)))
 void step_kernel_blockdyn(State<R> S, IO<R> io) { step_body_blockdyn<R, MODE, EPW, LID>(S, io); }
 
 // ---- block-queue step (f32 window lidar, cap <= 32): 1024-thread blocks of 16 waves own
@@ -1968,18 +1934,9 @@ void step_kernel_blockdyn(State<R> S, IO<R> io) { step_body_blockdyn<R, MODE, EP
 // before the sensors reach them).
 // Each wave's first pair is static (pair = wave); its rows and the next pair's are DMA'd while
 // the current pair is scanned (one DMA instruction per pair: two 384-B SoA rows).
-#ifndef USV_QE
-#define USV_QE 128       // envs per block-queue block (diagnostic builds may change it)
-#endif
-#ifndef USV_QW
-#define USV_QW 16        // waves per block-queue block (diagnostic builds may change it)
-#endif
-#ifndef USV_QSGPR
-#define USV_QSGPR 80     // SGPR budget of the block-queue kernel (80: 8 waves per SIMD)
-#endif
-#ifndef USV_QWPE
-#define USV_QWPE 8       // waves per SIMD it is compiled for
-#endif
+// kQE = 128 envs on kQW = 16 waves per block-queue block, compiled for 8 waves per SIMD (kQWPE) in
+// kQSgpr = 80 SGPRs
+constexpr int kQSgpr = 80, kQWPE = 8;
 // Issue priority in the block queue (round 5).  VALU issue on a SIMD goes by priority, then age, so a
 // CU's older block (the first one dispatched to it) wins every tie against the younger one: in the
 // round-4 timeline the older block ended at ~11.7 us and the younger ran alone, at 4 waves per SIMD,
@@ -1991,14 +1948,8 @@ void step_kernel_blockdyn(State<R> S, IO<R> io) { step_body_blockdyn<R, MODE, EP
 // with more rounds (524 288 envs) the phase-1 priority cost 0.9 us of 161.  Same-box A/Bs (gpurun_out
 // r5b-r5e): -0.27 to -0.67 us per launch at 65 536 envs (usv-simple), -0.95 us (usv-asmc-simple, whose
 // q kernel has the same phase 1).
-#ifndef USV_QPRIO_DYN
-#define USV_QPRIO_DYN 3
-#endif
-#ifndef USV_QPRIO_YOUNG
-#define USV_QPRIO_YOUNG 10
-#endif
-constexpr int kQYoungWaves = USV_QPRIO_YOUNG;
-constexpr int kQW = USV_QW, kQE = USV_QE, kQRec = 16;
+constexpr int kQPrioDyn = 3, kQYoungWaves = 10;
+constexpr int kQW = 16, kQE = 128, kQRec = 16;
 __host__ __device__ constexpr size_t q_slice_bytes() { return 256 * 8 + 64 * 4 + 2 * 1024; }
 
 // One DMA instruction (<= 64 pieces of 16 B, i.e. <= 1 KiB): pieces c >= nchunk are not copied.
@@ -2074,10 +2025,7 @@ __device__ __forceinline__ void q_emit_done(const State<float>& S, const IO<floa
 // Two block shapes: QE = 128 envs on QW = 16 waves (the default, two blocks per CU), and QE = 16 envs
 // on QW = 8 waves for small env counts, where 128-env blocks would leave most CUs idle (4 096 envs
 // are 32 such blocks) -- each wave then owns about one pair, and up to four blocks share a CU.
-#ifndef USV_QE_S
-#define USV_QE_S 16      // envs per small block (diagnostic builds may change it)
-#endif
-constexpr int kQE_S = USV_QE_S, kQW_S = 8;
+constexpr int kQE_S = 16, kQW_S = 8;
 constexpr int kQSmallBelow = 32768;   // env count below which the small blocks are the default (tools/nsweep.sh)
 template <int QE = kQE, int QW = kQW> __host__ __device__ constexpr size_t lds_q_bytes() {
   return wave_tab_bytes<float>() + QW * q_slice_bytes() + QE * kQRec * 4 + 16 + QE * 4;   // + n_obs[QE]
@@ -2161,9 +2109,7 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
     // every lane loads the state before any lane stores it); a wave with no env of its own must
     // not run, or two waves would race on the same env's state
     if (wave < kDynWaves && wave * kWave < nbe) {
-#if USV_QPRIO_DYN
-      if (S.qyoung != INT_MAX) __builtin_amdgcn_s_setprio(USV_QPRIO_DYN);
-#endif
+      if (S.qyoung != INT_MAX) __builtin_amdgcn_s_setprio(kQPrioDyn);
       const int k = min(wave * kWave + l, nbe - 1);
       const int e = eb + k;
       const float2 a = reinterpret_cast<const float2*>(io.act)[e];
@@ -2185,11 +2131,8 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
   if (wave >= kDynWaves) vm_wait<0>();
   QMARK(10);
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#if USV_QPRIO_DYN
   if (FUSED && wave < kDynWaves) __builtin_amdgcn_s_setprio(0);
-#endif
   if ((int)blockIdx.x >= S.qyoung && wave < kQYoungWaves) __builtin_amdgcn_s_setprio(1);
-#if USV_QFLAG
   // Same-step reset ordering: a dynamics wave stored its envs' state in phase 1, and
   // another wave may reset one of those envs later in this launch; two waves' stores to one address
   // are ordered only if the first is acknowledged before the second is issued.  So each dynamics
@@ -2202,7 +2145,6 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
     vm_wait<0>();
     __hip_atomic_store(qdyn + wave, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
-#endif
   USV_STAMP_W(2);
   QMARK(0);
   unsigned tk = 0;
@@ -2277,11 +2219,7 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
       if (nxt >= np) nxt = -1;
       if (nxt >= 0) {                                  // wave-uniform
         if (l == 0) tk = atomicAdd(qctr, 1u);
-#ifdef USV_DMA_ROW64
-        dma_copy1(S.orow(eb + 2 * nxt), nbuf, (pair_hasb(nxt) ? 2 : 1) * rowb);
-#else
         dma_copy_at(oblk, 2 * rowb * nxt, nbuf, (pair_hasb(nxt) ? 2 : 1) * rowb);
-#endif
       }
       // this lane's env: lanes 0..31 env A, 32..63 env B (env A again when there is no B)
       const int kl = (hb && hasB) ? k0 + 1 : k0;
@@ -2378,7 +2316,7 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
     QMARK(11);
     for (; done; done &= done - 1) {
       const int e = de0 + __builtin_ctz(done);
-      if constexpr (FUSED && USV_QFLAG) {
+      if constexpr (FUSED) {
         // the env's phase-1 stores (by dynamics wave (e - eb) / 64) are acknowledged before its reset
         // stores are issued: two waves' stores to one address are otherwise unordered
         const unsigned* const f = qdyn + ((e - eb) >> 6);
@@ -2399,7 +2337,7 @@ __device__ __forceinline__ void step_q_body(const State<float>& S, const IO<floa
 }
 
 template <int MODE, bool FUSED, bool DONE, bool CHAIN = true, bool INFO = false, bool SPAN = false>
-__global__ __launch_bounds__(kQW * kWave) __attribute__((amdgpu_num_sgpr(USV_QSGPR), amdgpu_waves_per_eu(USV_QWPE, USV_QWPE)))
+__global__ __launch_bounds__(kQW * kWave) __attribute__((amdgpu_num_sgpr(kQSgpr), amdgpu_waves_per_eu(kQWPE, kQWPE)))
 void step_q_kernel(State<float> S, IO<float> io) { step_q_body<MODE, FUSED, DONE, kQE, kQW, CHAIN, INFO, SPAN>(S, io); }
 template <int MODE, bool DONE, bool CHAIN = true, bool INFO = false>
 __global__ __launch_bounds__(kQW_S * kWave) __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(8, 8)))
@@ -3543,7 +3481,7 @@ int usv_create(const usv_config* cfg, int32_t device, void** out) {
     // at 65 536 envs: 40.3 us, against 47.7 for the split dyn_kernel + scan), else 8
     h->kind = 3; h->epb = cfg->num_envs >= 49152 ? 64 : 32;
   } else { h->kind = 1; h->epb = 64; }
-  h->prio = h->kind >= 4 ? 0 : USV_STATIC_PRIO;   // the ramp helps static splits only
+  h->prio = h->kind >= 4 ? 0 : kStaticPrio;   // the ramp helps static splits only
   if (const int rc = queue_lds_attr(h); rc != USV_OK) { delete h; return rc; }
   const int rc = cfg->precision == USV_F32 ? carve<float>(h, h->sf) : carve<double>(h, h->sd);
   if (rc != USV_OK) {
@@ -3583,7 +3521,7 @@ int usv_set_kernel_variant(void* hp, int32_t kind, int32_t epb, int32_t lid) {
   h->kind = kind;
   h->epb = epb;
   h->lid = lid;
-  h->prio = kind >= 4 ? 0 : USV_STATIC_PRIO;
+  h->prio = kind >= 4 ? 0 : kStaticPrio;
   h->sf.prio = h->sd.prio = h->prio;
   h->sf.rowspan = h->sd.rowspan = rs ? rs == 0x100 : h->cfg.num_envs >= kRowSpanFrom;
   return USV_OK;
