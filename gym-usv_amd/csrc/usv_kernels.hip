@@ -201,9 +201,9 @@ template <> struct Vec2<double> { using T = double2; };
 
 // obs[0:15] = [velocity/10, target_state(4), last_action[[0,2]]/max_action[[0,2]],
 //              max_action/10, max_acceleration/10]   (simple_env.py:72-96)
-// x / c for a compile-time constant c: exact division in the f64 build, a multiply by the
+// x / c for a compile-time constant c: correctly rounded in the f64 build (div_const), a multiply by the
 // rounded reciprocal (<= 1 ulp) in the f32 build.
-template <typename R> __device__ __forceinline__ R cdiv(R x, double c) { return x / R(c); }
+template <typename R> __device__ __forceinline__ R cdiv(R x, double c) { return div_const(x, c); }
 template <> __device__ __forceinline__ float cdiv(float x, double c) { return x * (float)(1.0 / c); }
 
 template <typename R>
