@@ -118,7 +118,7 @@ def test_committed_counters_cover_the_driver_line():
                 "usv-simple/524288/f32/window"):
         assert all(bench.pmc_entry(pmc, key)), key
     assert bench.pmc_entry(pmc, "no/such/key") == (None, None)
-    assert json.load(open(pmc))["usv-simple/65536/f32/window"]["round"].startswith("r05")
+    assert json.load(open(pmc))["usv-simple/65536/f32/window"]["round"].startswith("r06")
 
 
 # --------------------------------------------------------------------------- bench.py --gpus N launcher
