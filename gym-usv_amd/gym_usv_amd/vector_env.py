@@ -80,7 +80,7 @@ def _ptr(t):
 class _OutSet:
     """A copy=True output set (UsvVectorEnv._fresh_outputs): the tensors, their storage, ctypes
     pointers, the reference-state baseline, and whether a tensor of it was recorded on a stream."""
-    __slots__ = ("ts", "st", "ptrs", "base", "exposed", "__weakref__")
+    __slots__ = ("ts", "tl", "st", "ptrs", "base", "exposed", "__weakref__")
 
     @classmethod
     def make(cls, n, d, dev, rdt, info_enabled):
@@ -97,6 +97,7 @@ class _OutSet:
         ent.ts = (obs_b.view(torch.float32).view(n, d), rew_b.view(rdt), term, trunc, done,
                   fobs_b.view(torch.float32).view(n, d),
                   info_bytes.view(rdt).view(n, _lib.INFO_DIM) if info_enabled else None)
+        ent.tl = tuple(t for t in ent.ts if t is not None)
         ent.st = buf.untyped_storage()
         ent.ptrs = tuple(_ptr(t) for t in ent.ts)
         ent.base, ent.exposed = None, False
@@ -109,10 +110,28 @@ class _OutSet:
                 t.record_stream = _retiring_record_stream(weakref.ref(t), wself)
         return ent
 
-    def state(self, own=()):
-        ts = self.ts
-        return (sys.getrefcount(ts), tuple(sys.getrefcount(t) - own.count(id(t)) for t in ts if t is not None),
-                tuple(t._use_count() for t in ts if t is not None), _STORAGE_USE_COUNT(self.st._cdata))
+    def state(self, h0, h1, h2):
+        """Reference counts of the set: the tuple, each tensor (less the env's own references, whose
+        ids are h0..h2), each tensor's TensorImpl, the storage."""
+        out = [sys.getrefcount(self.ts), _STORAGE_USE_COUNT(self.st._cdata)]
+        for t in self.tl:
+            i = id(t)
+            out.append(sys.getrefcount(t) - (i == h0) - (i == h1) - (i == h2))
+            out.append(t._use_count())
+        return out
+
+    def unchanged(self, h0, h1, h2):
+        """state(h0, h1, h2) == base, stopping at the first difference."""
+        b = self.base
+        if sys.getrefcount(self.ts) != b[0] or _STORAGE_USE_COUNT(self.st._cdata) != b[1]:
+            return False
+        k = 2
+        for t in self.tl:
+            i = id(t)
+            if sys.getrefcount(t) - (i == h0) - (i == h1) - (i == h2) != b[k] or t._use_count() != b[k + 1]:
+                return False
+            k += 2
+        return True
 
 
 def _retiring_record_stream(wt, wset):
@@ -367,9 +386,9 @@ class UsvVectorEnv:
             # the env's own references to the last step's outputs (reset(mask=) keeps the rows of the
             # envs it does not reset) are not the caller's: ids, so that reading them adds none
             d = self.__dict__
-            own = (id(d.get("_last_obs")), id(d.get("_last_rew")), id(d.get("info_buf")))
+            h0, h1, h2 = id(d.get("_last_obs")), id(d.get("_last_rew")), id(d.get("info_buf"))
             for ent in ring:
-                if not ent.exposed and ent.state(own) == ent.base:
+                if not ent.exposed and ent.unchanged(h0, h1, h2):
                     return ent.ts, ent.ptrs
         ent = _OutSet.make(self.num_envs, self.obs_dim, self.device, self._rdt, self.info_enabled)
         if len(ring) >= self._RING:
@@ -377,7 +396,7 @@ class UsvVectorEnv:
         ring.append(ent)
         ring[:] = [e for e in ring if not e.exposed]   # retired sets: the allocator's from now on
         if _STORAGE_USE_COUNT is not None:
-            ent.base = ent.state()
+            ent.base = ent.state(0, 0, 0)
         return ent.ts, ent.ptrs
 
     def step_raw(self, actions, obs, reward, term, trunc, final_obs=None, stream=None):
