@@ -576,7 +576,8 @@ def run(args, rank, world, local, workload_cls=None):
             "steps": K, "warmup": W, "clock_warmup_steps": extra, "ms_per_step": round(elapsed / K * 1e3, 5),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "ranks_seen": ranks_seen,
             "launcher": os.environ.get("USV_BENCH_LAUNCHER",
-                                       "torch.distributed.run" if world > 1 else "single process"),
+                                       "torch.distributed.run" if world > 1 or "TORCHELASTIC_RUN_ID" in os.environ
+                                       else "single process"),
             "dtype": args.precision, "data": "synthetic (on-device uniform random actions, Philox env resets)",
             "config": {"workload": f"C3: {args.env_id}, {N} envs per GPU, random-action rollout, "
                                    f"in-kernel TimeLimit + same-step autoreset",

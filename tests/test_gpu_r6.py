@@ -164,3 +164,26 @@ def test_asmc_compute_rejects_host_pointers():
                                 vp(st.data_ptr()), None, 0, 1, s0) == 0
     torch.cuda.synchronize()
     assert torch.isfinite(pos).all()
+
+
+def test_bench_line_at_n1_has_the_contract_fields():
+    """python bench.py --gpus 1 (short): one JSON line with the contract's fields, the roofline and
+    API objects, one rank, a single-process launcher (the driver's N = 1 form)."""
+    import json
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1", "--steps", "20",
+                        "--warmup", "5", "--no-cpu-baseline", "--f64-steps", "50", "--api-steps", "20",
+                        "--steady-steps", "100"], capture_output=True, text=True, env=env, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["ranks_seen"] == 1 and d["launcher"] == "single process"
+    assert d["steps"] == 20 and d["value"] > 0 and d["scaling"] == "weak"
+    r = d["roofline"]
+    assert r["bound"] == "hbm" and 0 < r["frac"] < 1 and r["unit"] == "GB/s" and r["peak"] == 8000.0
+    assert d["config"]["envs_per_gpu"] == 65536 and d["f64"]["dtype"] == "f64"
+    assert d["value"] == pytest.approx(65536 * 20 / (d["ms_per_step"] * 20 / 1e3), rel=1e-3)
