@@ -12,6 +12,7 @@ from __future__ import annotations
 import ctypes
 import sys
 import warnings
+import weakref
 
 import numpy as np
 import torch
@@ -84,7 +85,6 @@ class _OutSet:
 
     @classmethod
     def make(cls, n, d, dev, rdt, info_enabled):
-        import weakref
         ent = cls()
         rb = torch.empty((), dtype=rdt).element_size()
         ob = n * d * 4
@@ -101,13 +101,8 @@ class _OutSet:
         ent.st = buf.untyped_storage()
         ent.ptrs = tuple(_ptr(t) for t in ent.ts)
         ent.base, ent.exposed = None, False
-        wself = weakref.ref(ent)
-        for t in ent.ts:
-            if t is not None:
-                # the tensor's record_stream, which also retires the set from the ring (instance
-                # attribute: it shadows Tensor.record_stream for this tensor only; weak references,
-                # so neither the tensor nor the set gains a reference)
-                t.record_stream = _retiring_record_stream(weakref.ref(t), wself)
+        _install_record_stream_hook()
+        _RING_SETS[ent.st.data_ptr()] = ent            # (weak: the entry goes with the set)
         return ent
 
     def state(self, h0, h1, h2):
@@ -134,13 +129,28 @@ class _OutSet:
         return True
 
 
-def _retiring_record_stream(wt, wset):
-    def record_stream(stream):
-        s = wset()
-        if s is not None:
-            s.exposed = True
-        return torch.Tensor.record_stream(wt(), stream)
-    return record_stream
+# Storage address -> live copy=True output set.  Tensor.record_stream is wrapped once (the first time a
+# set is made) so that recording any tensor or view of a set's storage on a stream retires that set from
+# the ring; the original method then runs unchanged.  A class-level wrapper, not a per-tensor attribute:
+# the outputs stay plain tensors (pickling, deepcopy and views behave as usual).
+_RING_SETS = weakref.WeakValueDictionary()
+_RECORD_STREAM = None
+
+
+def _install_record_stream_hook():
+    global _RECORD_STREAM
+    if _RECORD_STREAM is not None:
+        return
+    orig = _RECORD_STREAM = torch.Tensor.record_stream
+
+    def record_stream(self, stream):
+        if _RING_SETS:
+            ent = _RING_SETS.get(self.untyped_storage().data_ptr())
+            if ent is not None:
+                ent.exposed = True
+        return orig(self, stream)
+    record_stream.__doc__ = orig.__doc__
+    torch.Tensor.record_stream = record_stream
 
 
 class UsvVectorEnv:
@@ -375,7 +385,7 @@ class UsvVectorEnv:
             same code at creation and at reuse, so the interpreter's own counting cancels out);
           * no other view of the storage (the storage use count);
           * no C++ holder of a tensor (TensorImpl use count: a DLPack capsule, an autograd graph);
-          * no other stream recorded on a tensor: ``record_stream`` on a handed-out tensor retires its
+          * no other stream recorded on it: ``record_stream`` on a handed-out tensor (or a view) retires its
             set from the ring for good, so the caching allocator frees it only after that stream's
             work, exactly as for any tensor it owns.
         Otherwise a new set is allocated: the caller always gets tensors that alias nothing it holds

@@ -325,6 +325,18 @@ def test_copy_outputs_held_by_dlpack_or_recorded_on_a_stream_are_not_reused_cpu(
         pass
     ring = f._out_ring
     assert any(e.exposed for e in ring)
+    # the outputs stay plain tensors: picklable, no per-tensor attributes (the hook is class-level)
+    import io
+    torch.save(ts3[0], io.BytesIO())
+    assert not ts3[0].__dict__
+    other = next((e for e in ring if not e.exposed), None)
+    if other is not None:                      # a view of another set's storage retires that set too
+        try:
+            other.ts[0][:, :15].record_stream(None)
+        except Exception:
+            pass
+        assert other.exposed
+    del other
     del ts3, _
     held = []
     for _ in range(4):                         # the recorded set never comes back from the ring
