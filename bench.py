@@ -355,20 +355,26 @@ def spawn_ranks(n, argv, target=_rank_entry, port=None):
     ctx = mp.get_context("spawn")
     port = port or _free_port()
     procs = [ctx.Process(target=target, args=(r, n, port, list(argv)), name=f"bench-rank{r}") for r in range(n)]
-    for p in procs:
-        p.start()
-    rc, live = 0, list(procs)
-    while live:
-        wait([p.sentinel for p in live])
-        for p in [p for p in live if not p.is_alive()]:
-            p.join()
-            live.remove(p)
-            if p.exitcode != 0 and rc == 0:
-                rc = p.exitcode if p.exitcode > 0 else 1
-                print(f"bench.py: {p.name} exited with status {p.exitcode}; stopping the other ranks",
-                      file=sys.stderr, flush=True)
-                for q in live:
-                    q.terminate()
+    rc, live = 0, []
+    try:
+        for p in procs:
+            p.start()
+            live.append(p)
+        while live:
+            wait([p.sentinel for p in live])
+            for p in [p for p in live if not p.is_alive()]:
+                p.join()
+                live.remove(p)
+                if p.exitcode != 0 and rc == 0:
+                    rc = p.exitcode if p.exitcode > 0 else 1
+                    print(f"bench.py: {p.name} exited with status {p.exitcode}; stopping the other ranks",
+                          file=sys.stderr, flush=True)
+                    for q in live:
+                        q.terminate()
+    finally:                       # (an interrupted parent leaves no rank behind)
+        for q in live:
+            q.terminate()
+            q.join(30)
     return rc
 
 
