@@ -187,3 +187,32 @@ def test_bench_line_at_n1_has_the_contract_fields():
     assert r["bound"] == "hbm" and 0 < r["frac"] < 1 and r["unit"] == "GB/s" and r["peak"] == 8000.0
     assert d["config"]["envs_per_gpu"] == 65536 and d["f64"]["dtype"] == "f64"
     assert d["value"] == pytest.approx(65536 * 20 / (d["ms_per_step"] * 20 / 1e3), rel=1e-3)
+
+
+@pytest.mark.parametrize("env_id", ["usv-simple", "usv-asmc-simple"])
+def test_max_size_batch_matches_its_shard(env_id):
+    """2^23 envs on one GPU (~20 GB of HBM for the state and the persistent outputs): the last 4 096 envs
+    of the batch step bit-identically to a 4 096-env batch with env_id_offset = N - 4096 (resets keyed by
+    global id; a 3-step TimeLimit so every env resets twice), i.e. no indexing overflows at the top of the
+    range and the DRAM-size kernel (row spans, multi-round grid) agrees with the small-count one."""
+    N, n, T = 1 << 23, 4096, 7
+    big = make(env_id, N, seed=21, max_episode_steps=3, copy=False)
+    small = make(env_id, n, seed=21, max_episode_steps=3, copy=False, env_id_offset=N - n)
+    ob, _ = big.reset(seed=21)
+    os_, _ = small.reset(seed=21)
+    assert torch.equal(ob[N - n:], os_)
+    gen = torch.Generator(device="cuda").manual_seed(9)
+    for t in range(T):
+        a = rand_actions(N, gen)
+        ob, rb, tb, trb, ib = big.step(a)
+        os_, rs, ts, trs, is_ = small.step(a[N - n:].contiguous())
+        torch.cuda.synchronize()
+        assert torch.equal(ob[N - n:], os_), f"obs differ at step {t}"
+        assert torch.equal(rb[N - n:], rs) and torch.equal(tb[N - n:], ts) and torch.equal(trb[N - n:], trs)
+        done = ib["_final_obs"][N - n:]
+        assert torch.equal(done, is_["_final_obs"])
+        if bool(done.any()):
+            assert torch.equal(ib["final_obs"][N - n:][done], is_["final_obs"][done])
+    assert bool(torch.isfinite(ob).all()) and bool(torch.isfinite(rb).all())
+    big.close()
+    small.close()
