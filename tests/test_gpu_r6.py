@@ -216,3 +216,22 @@ def test_max_size_batch_matches_its_shard(env_id):
     assert bool(torch.isfinite(ob).all()) and bool(torch.isfinite(rb).all())
     big.close()
     small.close()
+
+
+def test_spawned_rank_runs_the_real_bench():
+    """bench.spawn_ranks with one rank on the real GPU (the machinery `--gpus N > 1` uses on a
+    multi-GPU node, here at N = 1): the spawned interpreter gets the launcher environment, binds
+    cuda:0, runs the timed window and prints the line; the parent returns its exit status."""
+    import json
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    argv = ["--gpus", "1", "--steps", "20", "--warmup", "5", "--no-cpu-baseline", "--f64-steps", "0",
+            "--api-steps", "0", "--steady-steps", "0"]
+    prog = ("import sys; sys.path.insert(0, %r); import bench; sys.exit(bench.spawn_ranks(1, %r))" % (ROOT, argv))
+    p = subprocess.run([sys.executable, "-c", prog], capture_output=True, text=True, env=env, timeout=300,
+                       cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["launcher"] == "bench.py spawn" and d["ranks_seen"] == 1 and d["n_gpus"] == 1
+    assert d["value"] > 0 and 0 < d["roofline"]["frac"] < 1
