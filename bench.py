@@ -347,8 +347,9 @@ def _rank_entry(rank, world, port, argv):
 
 
 def spawn_ranks(n, argv, target=_rank_entry, port=None):
-    """Start n rank processes (multiprocessing "spawn": fresh interpreters, nothing forked from or
-    exec'd over this process, which has made no GPU call) and wait for them.  Returns 0, or the exit
+    """Start n rank processes (multiprocessing "spawn": each child execs a fresh interpreter at once, so
+    no rank inherits this process's state, and nothing is exec'd over this process, which has made no
+    GPU call) and wait for them.  Returns 0, or the exit
     status of the first rank that fails, after terminating the others (a rank left waiting in a
     barrier for a dead peer would otherwise hang)."""
     from multiprocessing.connection import wait
