@@ -139,3 +139,23 @@ def test_integration_snippet_runs_verbatim_to_create(lib):
     import torch
     if not torch.cuda.is_available():
         assert line.split()[1] != "0" and len(line.split()) > 2, line
+
+
+def test_div_const_is_ieee_division_on_host(tmp_path):
+    """div_const (usv_device.hpp), the f64 build's division by compile-time constants, restated in C with
+    the same fma sequence: equal to x / c for 1e6 random operands per divisor (tools/micro/div_const_check.c;
+    round 6 ran 2e8 per divisor)."""
+    import os
+    import shutil
+    import subprocess
+    cc = shutil.which("gcc")
+    if cc is None:
+        import pytest
+        pytest.skip("no gcc")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = str(tmp_path / "div_const_check")
+    subprocess.run([cc, "-O2", "-ffp-contract=off", "-o", exe, os.path.join(root, "tools", "micro", "div_const_check.c"),
+                    "-lm"], check=True)
+    p = subprocess.run([exe, "1000000"], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stdout
+    assert p.stdout.count(": 0 mismatches") == 10
